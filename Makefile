@@ -1,0 +1,39 @@
+# Builds every native artefact in-tree (they travel to the GPU box with the snapshot).
+#   blt_amd/libblt_bpe.so    product: HIP kernels for gfx950 + C ABI host library
+#   blt_amd/libblt_synth.so  seeded synthetic workloads (bench / tests)
+#   blt_amd/blt              CLI drop-in for the reference `blt` binary
+#   oracle/liboracle.so      CPU restatement of the reference (test infrastructure only)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+CC ?= gcc
+
+LIB := blt_amd/libblt_bpe.so
+SYNTH := blt_amd/libblt_synth.so
+ORACLE := oracle/liboracle.so
+OBJDIR := build
+
+all: $(LIB) $(SYNTH) $(ORACLE)
+
+$(OBJDIR):
+	mkdir -p $(OBJDIR)
+
+$(OBJDIR)/bpe_kernels.o: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/blt_host.o: blt_amd/csrc/blt_host.cpp blt_amd/csrc/bpe_kernels.h include/blt_bpe.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJDIR)/bpe_kernels.o $(OBJDIR)/blt_host.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -lpthread
+
+$(SYNTH): blt_amd/csrc/synth.c
+	$(CC) -O2 -fPIC -fopenmp -shared -o $@ $<
+
+$(ORACLE): oracle/bpe_oracle.c
+	$(MAKE) -C oracle liboracle.so
+
+clean:
+	rm -rf $(OBJDIR) $(LIB) $(SYNTH) $(ORACLE)
+
+.PHONY: all clean

@@ -1,0 +1,213 @@
+"""blt_amd — MI355X-native BPE merge scan, a drop-in for jtrefon/blt's BPE strategy path.
+
+Python mirror of the reference's strategy surface over the C ABI in include/blt_bpe.h:
+
+* ``TokenizationStrategy.process_chunk(chunk) -> bytes``   (blt_core/src/tokenizer.rs:21-31)
+* ``BpeStrategy(merges)`` / ``BpeStrategy.new(merges)``     (tokenizer.rs:43-93)
+* ``BasicTokenizationStrategy``                             (tokenizer.rs:96-124)
+* ``load_bpe_merges_from_path`` / ``load_bpe_merges``       (config_loader.rs:14-46, lib.rs:216-230)
+* ``parse_chunk_size_str``, ``get_effective_chunk_size``, ``determine_thread_count``
+  (utils.rs:10-45, chunking.rs:26-62, utils.rs:79-97)
+* ``BpeStrategy.process_chunks(data, chunk_size, n_gpus)``  — the mmap pipeline's chunk split and
+  ordered stitch (pipeline.rs:56-192), sharded over GPUs.
+
+All tokenising calls run the HIP kernels in libblt_bpe.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+from . import _lib
+from ._lib import BltError
+
+__all__ = [
+    "BltError", "TokenizationStrategy", "BpeStrategy", "BasicTokenizationStrategy", "ContentType",
+    "load_bpe_merges_from_path", "load_bpe_merges", "parse_chunk_size_str", "get_effective_chunk_size",
+    "determine_thread_count", "version",
+]
+
+
+def version() -> str:
+    return _lib.lib().blt_version().decode()
+
+
+class ContentType:
+    """ContentType::get_token_value — blt_core/src/lib.rs:93-104."""
+    Text = 0xFF01
+    Audio = 0xFF02
+    Bin = 0xFF03
+    Video = 0xFF04
+    BY_NAME = {"text": Text, "audio": Audio, "bin": Bin, "video": Video}
+
+
+def _buf(data):
+    """(address, length, keepalive) of a bytes-like / numpy uint8 object."""
+    try:
+        import numpy as np
+        if isinstance(data, np.ndarray):
+            a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+            return a.ctypes.data, a.size, a
+    except ImportError:  # pragma: no cover
+        pass
+    mv = memoryview(data).cast("B")
+    if mv.readonly:
+        b = ctypes.create_string_buffer(bytes(mv), max(len(mv), 1))
+        return ctypes.addressof(b), len(mv), b
+    b = (ctypes.c_uint8 * max(len(mv), 1)).from_buffer(mv) if len(mv) else (ctypes.c_uint8 * 1)()
+    return ctypes.addressof(b), len(mv), (b, mv)
+
+
+def load_bpe_merges_from_path(path: str) -> Dict[Tuple[int, int], int]:
+    """config_loader.rs:14-46.  Raises BltError (kind NotFound / InvalidData / Other)."""
+    L = _lib.lib()
+    cap = 65536
+    A = (ctypes.c_uint16 * cap)()
+    B = (ctypes.c_uint16 * cap)()
+    V = (ctypes.c_uint16 * cap)()
+    n = ctypes.c_size_t(0)
+    _lib.check(L.blt_load_bpe_merges(str(path).encode(), A, B, V, cap, ctypes.byref(n)))
+    return {(A[i], B[i]): V[i] for i in range(n.value)}
+
+
+def load_bpe_merges(path: str) -> Dict[Tuple[int, int], int]:
+    """blt_core::load_bpe_merges (lib.rs:216-230): the file's map with (u8, u8) keys."""
+    return {k: v for k, v in load_bpe_merges_from_path(path).items() if k[0] <= 255 and k[1] <= 255}
+
+
+def parse_chunk_size_str(s: str) -> int:
+    """utils.rs:10-45.  Raises ValueError with the reference's message."""
+    out = ctypes.c_uint64(0)
+    L = _lib.lib()
+    if L.blt_parse_chunk_size(s.encode(), ctypes.byref(out)) != 0:
+        raise ValueError(L.blt_last_error().decode())
+    return out.value
+
+
+def get_effective_chunk_size(cli_chunk_size: Optional[int], num_threads: int, mem_cap_percent: int = 80) -> int:
+    """chunking.rs:26-62 (dynamic branch reads /proc/meminfo, like sysinfo's total_memory)."""
+    return _lib.lib().blt_effective_chunk_size(int(cli_chunk_size is not None), cli_chunk_size or 0,
+                                               num_threads, mem_cap_percent)
+
+
+def determine_thread_count(threads: Optional[int]) -> int:
+    """utils.rs:79-97."""
+    return _lib.lib().blt_determine_thread_count(int(threads is not None), threads or 0)
+
+
+class TokenizationStrategy:
+    """trait TokenizationStrategy (tokenizer.rs:21-31): process one chunk of bytes."""
+
+    def process_chunk(self, chunk_data) -> bytes:  # pragma: no cover - interface
+        raise NotImplementedError
+
+
+class BpeStrategy(TokenizationStrategy):
+    """BpeStrategy (tokenizer.rs:33-94) on the GPU.
+
+    ``merges`` is a BpeMerges map {(u16, u16): u16} (lib.rs:75).  The handle is immutable and
+    safe to share between threads, like the reference's Arc<dyn TokenizationStrategy>.
+    """
+
+    def __init__(self, merges: Optional[Dict[Tuple[int, int], int]] = None, *, _handle=None):
+        self._L = _lib.lib()
+        self._h = ctypes.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            items = list((merges or {}).items())
+            n = len(items)
+            A = (ctypes.c_uint16 * max(n, 1))(*[int(k[0]) for k, _ in items])
+            B = (ctypes.c_uint16 * max(n, 1))(*[int(k[1]) for k, _ in items])
+            V = (ctypes.c_uint16 * max(n, 1))(*[int(v) for _, v in items])
+            _lib.check(self._L.blt_bpe_create(A, B, V, n, 0, ctypes.byref(self._h)))
+
+    @classmethod
+    def new(cls, bpe_merges: Dict[Tuple[int, int], int]) -> "BpeStrategy":
+        """BpeStrategy::new(Arc<BpeMerges>) — tokenizer.rs:48."""
+        return cls(bpe_merges)
+
+    @classmethod
+    def from_file(cls, merges_path: str) -> "BpeStrategy":
+        """CoreConfig::load_bpe_data + select_strategy (lib.rs:184-201, :271-282)."""
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(L.blt_bpe_create_from_file(str(merges_path).encode(), ctypes.byref(h)))
+        return cls(_handle=h)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.blt_bpe_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover
+            pass
+
+    @property
+    def handle(self) -> int:
+        return self._h.value
+
+    def info(self) -> Tuple[int, bool]:
+        n = ctypes.c_size_t(0)
+        sp = ctypes.c_int(0)
+        _lib.check(self._L.blt_bpe_info(self._h, ctypes.byref(n), ctypes.byref(sp)))
+        return n.value, bool(sp.value)
+
+    def process_chunk(self, chunk_data) -> bytes:
+        """TokenizationStrategy::process_chunk (tokenizer.rs:56-93): BE u16 token bytes."""
+        ptr, n, keep = _buf(chunk_data)
+        out = ctypes.create_string_buffer(max(2 * n, 1))
+        olen = ctypes.c_size_t(0)
+        _lib.check(self._L.blt_bpe_process_chunk(self._h, ptr, n, out, 2 * n, ctypes.byref(olen)))
+        return out.raw[:olen.value]
+
+    def process_chunks(self, data, chunk_size: int, n_gpus: int = 1, return_chunk_lens: bool = False):
+        """Chunk split + per-chunk BPE + ordered concatenation (pipeline.rs:73-81, :153-192)."""
+        import numpy as np
+        ptr, n, keep = _buf(data)
+        out = np.empty(max(2 * n, 1), dtype=np.uint8)
+        nchunks = (n + chunk_size - 1) // chunk_size if n else 0
+        lens = np.zeros(max(nchunks, 1), dtype=np.uint64)
+        olen = ctypes.c_size_t(0)
+        _lib.check(self._L.blt_bpe_process_chunks(self._h, ptr, n, chunk_size, n_gpus, out.ctypes.data, 2 * n,
+                                                  ctypes.byref(olen), lens.ctypes.data))
+        res = out[:olen.value]
+        if return_chunk_lens:
+            return res, lens[:nchunks].astype(np.int64)
+        return res
+
+    # ---- device-resident API (pointers are integers, e.g. torch tensor .data_ptr()) ----
+    def workspace_size(self, n: int, chunk_size: int) -> int:
+        return self._L.blt_bpe_workspace_size(self._h, n, chunk_size)
+
+    def encode_device(self, d_in: int, n: int, chunk_size: int, d_out: int, d_workspace: int,
+                      workspace_bytes: int, stream: int = 0, d_chunk_off: int = 0, sync: bool = True):
+        """blt_bpe_encode_device: returns the token count when sync, else None (async enqueue)."""
+        tok = ctypes.c_uint64(0)
+        _lib.check(self._L.blt_bpe_encode_device(self._h, d_in, n, chunk_size, d_out, d_chunk_off or None,
+                                                 d_workspace, workspace_bytes, stream or None,
+                                                 ctypes.byref(tok) if sync else None))
+        return tok.value if sync else None
+
+    def check_workspace(self, d_workspace: int, stream: int = 0) -> None:
+        _lib.check(self._L.blt_bpe_check_workspace(d_workspace, stream or None))
+
+
+class BasicTokenizationStrategy(TokenizationStrategy):
+    """BasicTokenizationStrategy (tokenizer.rs:96-124) on the GPU: byte b -> BE [0, b]."""
+
+    def __init__(self):
+        self._L = _lib.lib()
+
+    def process_chunk(self, chunk_data) -> bytes:
+        ptr, n, keep = _buf(chunk_data)
+        out = ctypes.create_string_buffer(max(2 * n, 1))
+        olen = ctypes.c_size_t(0)
+        _lib.check(self._L.blt_basic_process_chunk(ptr, n, out, 2 * n, ctypes.byref(olen)))
+        return out.raw[:olen.value]
+
+    def encode_device(self, d_in: int, n: int, d_out: int, stream: int = 0) -> None:
+        _lib.check(self._L.blt_basic_encode_device(d_in, n, d_out, stream or None))

@@ -1,0 +1,777 @@
+// Host side of the MI355X BPE merge scan: the C ABI of include/blt_bpe.h.
+//
+// Owns the merges loader (config_loader.rs:14-46), the config helpers (utils.rs, chunking.rs),
+// the strategy handle (BpeStrategy, tokenizer.rs:43-93) with its device tables, the per-pass
+// orchestration of the kernels in bpe_kernels.hip, and the multi-GPU chunk sharding that
+// replaces the reference's tokio task-per-chunk pipeline (pipeline.rs:56-192).
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <fstream>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/blt_bpe.h"
+#include "bpe_kernels.h"
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(BLT_E_IO, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Text helpers for the loader: Rust's BufRead::lines() / str::split_whitespace / FromStr.
+// ---------------------------------------------------------------------------------------
+// Length of the UTF-8 sequence at p (code point in *cp), 0 if malformed.
+size_t utf8_seq(const unsigned char* p, size_t n, uint32_t* cp) {
+    if (!n) return 0;
+    const unsigned c = p[0];
+    if (c < 0x80) { *cp = c; return 1; }
+    size_t len = (c >= 0xF0 && c <= 0xF4) ? 4 : (c >= 0xE0) && c < 0xF0 ? 3 : (c >= 0xC2 && c < 0xE0) ? 2 : 0;
+    if (!len || len > n) return 0;
+    uint32_t v = c & (len == 2 ? 0x1F : len == 3 ? 0x0F : 0x07);
+    for (size_t i = 1; i < len; ++i) {
+        if ((p[i] & 0xC0) != 0x80) return 0;
+        v = (v << 6) | (p[i] & 0x3F);
+    }
+    static const uint32_t kMin[5] = {0, 0, 0x80, 0x800, 0x10000};
+    if (v < kMin[len] || v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) return 0;
+    *cp = v;
+    return len;
+}
+
+bool is_white_space(uint32_t c) {  // Unicode White_Space (char::is_whitespace)
+    switch (c) {
+        case 0x20: case 0x85: case 0xA0: case 0x1680: case 0x2028: case 0x2029: case 0x202F: case 0x205F:
+        case 0x3000: return true;
+        default: return (c >= 0x09 && c <= 0x0D) || (c >= 0x2000 && c <= 0x200A);
+    }
+}
+
+// Fields of str::split_whitespace over a valid UTF-8 line.
+std::vector<std::string> split_whitespace(const std::string& s) {
+    std::vector<std::string> out;
+    const auto* p = reinterpret_cast<const unsigned char*>(s.data());
+    size_t i = 0, start = 0;
+    bool in = false;
+    while (i < s.size()) {
+        uint32_t cp = 0;
+        size_t l = utf8_seq(p + i, s.size() - i, &cp);
+        if (!l) l = 1;
+        if (is_white_space(cp)) {
+            if (in) out.emplace_back(s, start, i - start);
+            in = false;
+        } else if (!in) {
+            in = true;
+            start = i;
+        }
+        i += l;
+    }
+    if (in) out.emplace_back(s, start);
+    return out;
+}
+
+// <uN as FromStr>::from_str in radix 10: optional sign handling of core::num for unsigned
+// types; per char the digit check comes before the overflow check.  "" on success, else the
+// ParseIntError text.
+const char* parse_unsigned(const std::string& s, uint64_t limit, uint64_t* out) {
+    if (s.empty()) return "cannot parse integer from empty string";
+    size_t i = 0;
+    if (s[0] == '+' || s[0] == '-') {
+        if (s.size() == 1) return "invalid digit found in string";
+        if (s[0] == '+') i = 1;
+    }
+    uint64_t r = 0;
+    for (; i < s.size(); ++i) {
+        const bool mul_ok = r <= limit / 10;
+        if (s[i] < '0' || s[i] > '9') return "invalid digit found in string";
+        if (!mul_ok) return "number too large to fit in target type";
+        r *= 10;
+        const uint64_t d = (uint64_t)(s[i] - '0');
+        if (r > limit - d) return "number too large to fit in target type";
+        r += d;
+    }
+    *out = r;
+    return "";
+}
+
+// load_bpe_merges_from_path (config_loader.rs:14-46) into a dense (a, b) -> id table
+// (-1 absent).  Returns 0 or a BLT_E_* code with t_err set to the io::Error text.
+int load_merges_table(const char* path, std::vector<int32_t>& table) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) {
+        const int e = errno ? errno : ENOENT;
+        return fail(e == ENOENT ? BLT_E_NOT_FOUND : BLT_E_IO, "%s (os error %d)", strerror(e), e);
+    }
+    std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (f.bad()) return fail(BLT_E_IO, "%s (os error %d)", strerror(EIO), EIO);
+    table.assign(65536, -1);
+    uint16_t vocab = 256;  // :18, wraps like the release build (no overflow-checks)
+    size_t pos = 0;
+    while (pos < data.size()) {
+        size_t nl = data.find('\n', pos);
+        const bool had_nl = nl != std::string::npos;
+        const size_t end = had_nl ? nl : data.size();
+        // read_line validates the bytes it appends, newline included
+        {
+            const auto* p = reinterpret_cast<const unsigned char*>(data.data()) + pos;
+            size_t i = 0, len = end - pos + (had_nl ? 1 : 0);
+            while (i < len) {
+                uint32_t cp;
+                size_t l = utf8_seq(p + i, len - i, &cp);
+                if (!l) return fail(BLT_E_INVALID_DATA, "stream did not contain valid UTF-8");
+                i += l;
+            }
+        }
+        std::string line = data.substr(pos, end - pos);
+        if (had_nl && !line.empty() && line.back() == '\r') line.pop_back();  // lines(): "\r\n"
+        pos = had_nl ? nl + 1 : end;
+        if (line.empty() || line[0] == '#') continue;  // :22
+        const std::vector<std::string> parts = split_whitespace(line);
+        if (parts.size() != 2)  // :41-43
+            return fail(BLT_E_INVALID_DATA,
+                        "Invalid merge rule format in line: '%s'. Expected two numbers separated by space.",
+                        line.c_str());
+        uint64_t b1 = 0, b2 = 0;
+        const char* e1 = parse_unsigned(parts[0], 255, &b1);
+        if (*e1) return fail(BLT_E_INVALID_DATA, "Failed to parse first byte value: %s in line '%s'", e1, line.c_str());
+        const char* e2 = parse_unsigned(parts[1], 255, &b2);
+        if (*e2) return fail(BLT_E_INVALID_DATA, "Failed to parse second byte value: %s in line '%s'", e2, line.c_str());
+        table[(b1 << 8) | b2] = vocab;  // :39 insert (last wins)
+        vocab = (uint16_t)(vocab + 1);   // :40
+    }
+    return 0;
+}
+
+uint64_t total_ram_bytes() {
+    FILE* f = fopen("/proc/meminfo", "r");
+    if (!f) return 0;
+    char key[64];
+    unsigned long long kb = 0;
+    uint64_t r = 0;
+    while (fscanf(f, "%63s %llu kB", key, &kb) == 2) {
+        if (strcmp(key, "MemTotal:") == 0) { r = (uint64_t)kb * 1024ull; break; }
+    }
+    fclose(f);
+    return r;
+}
+
+}  // namespace
+
+// ===========================================================================================
+// Strategy handle
+// ===========================================================================================
+constexpr int kMaxDevices = 64;
+
+struct DevTables {
+    std::once_flag once;
+    int status = 0;
+    uint16_t* dense = nullptr;
+    uint64_t* hslots = nullptr;
+};
+
+struct blt_bpe {
+    size_t n_entries = 0;
+    bool single_pass = true;
+    uint32_t sentinel = 0;                 // > 0xFFFF: every byte pair is a merge
+    std::vector<uint16_t> dense;           // 65536, swizzled (blt::dense_index)
+    std::vector<uint64_t> hslots;          // general map, empty when single_pass
+    uint64_t hmask = 0;
+    DevTables dev[kMaxDevices];
+};
+
+namespace {
+
+int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>& vals, blt_bpe** out) {
+    std::unique_ptr<blt_bpe> h(new (std::nothrow) blt_bpe());
+    if (!h) return fail(BLT_E_NOMEM, "out of host memory");
+    // Final map: later duplicates overwrite (HashMap collect).
+    std::unordered_map<uint32_t, uint16_t> map;
+    map.reserve(keys.size() * 2 + 1);
+    for (size_t i = 0; i < keys.size(); ++i) map[keys[i]] = vals[i];
+    h->n_entries = map.size();
+
+    // One pass is the fixpoint when no value is a key component: after pass 1 two adjacent
+    // raw bytes were adjacent in the input and already rejected, and a merged token can match
+    // no key.
+    std::vector<uint8_t> is_value(65536, 0), is_comp(65536, 0);
+    for (const auto& kv : map) {
+        is_value[kv.second] = 1;
+        is_comp[kv.first >> 16] = 1;
+        is_comp[kv.first & 0xFFFF] = 1;
+    }
+    for (int t = 0; t < 65536 && h->single_pass; ++t)
+        if (is_value[t] && is_comp[t]) h->single_pass = false;
+
+    // Dense byte-pair table for pass 1: value, or a sentinel no byte-pair key maps to.
+    std::vector<uint8_t> used(65536, 0);
+    size_t byte_pairs = 0;
+    for (const auto& kv : map)
+        if ((kv.first >> 16) < 256 && (kv.first & 0xFFFF) < 256) { used[kv.second] = 1; ++byte_pairs; }
+    if (byte_pairs == 65536) {
+        h->sentinel = 0x10000u;
+    } else {
+        uint32_t s = 0xFFFF;
+        while (used[s]) --s;  // at most 65535 values are used, so one is free
+        h->sentinel = s;
+    }
+    h->dense.assign(65536, (uint16_t)(h->sentinel & 0xFFFF));
+    for (const auto& kv : map) {
+        const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
+        if (a < 256 && b < 256) h->dense[blt::dense_index(a, b)] = kv.second;
+    }
+    if (!h->single_pass) {
+        uint64_t cap = 16;
+        while (cap < 2 * (uint64_t)map.size() + 2) cap <<= 1;
+        h->hslots.assign(cap, 0);
+        h->hmask = cap - 1;
+        for (const auto& kv : map) {
+            uint64_t s = blt::slot_hash(kv.first) & h->hmask;
+            while (h->hslots[s] >> 63) s = (s + 1) & h->hmask;
+            h->hslots[s] = (1ull << 63) | ((uint64_t)kv.second << 32) | kv.first;
+        }
+    }
+    *out = h.release();
+    return 0;
+}
+
+int current_device(int* dev) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return fail(BLT_E_NODEV, "no HIP device available");
+    HIP_TRY(hipGetDevice(dev));
+    if (*dev < 0 || *dev >= kMaxDevices) return fail(BLT_E_NODEV, "device index %d out of range", *dev);
+    return 0;
+}
+
+int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
+    blt_bpe* h = const_cast<blt_bpe*>(hc);
+    DevTables& t = h->dev[dev];
+    // Upload on a private stream and wait for it: the kernels run on non-blocking streams,
+    // which do not order behind null-stream copies.
+    std::call_once(t.once, [&]() {
+        hipStream_t us = nullptr;
+        bool ok = hipStreamCreateWithFlags(&us, hipStreamNonBlocking) == hipSuccess &&
+                  hipMalloc(&t.dense, 65536 * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.dense, h->dense.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice, us) ==
+                      hipSuccess;
+        if (ok && !h->hslots.empty()) {
+            const size_t bytes = h->hslots.size() * sizeof(uint64_t);
+            ok = hipMalloc(&t.hslots, bytes) == hipSuccess &&
+                 hipMemcpyAsync(t.hslots, h->hslots.data(), bytes, hipMemcpyHostToDevice, us) == hipSuccess;
+        }
+        ok = ok && hipStreamSynchronize(us) == hipSuccess;
+        if (us) (void)hipStreamDestroy(us);
+        if (!ok) t.status = BLT_E_IO;
+    });
+    if (t.status) return fail(t.status, "uploading merge tables to device %d failed", dev);
+    *out = &t;
+    return 0;
+}
+
+// Test hook: per-tile look-back records (blt_debug_set_tile_record).
+uint64_t* g_debug_tiles = nullptr;
+
+// ---- workspace layout -------------------------------------------------------------------
+inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
+
+struct WsLayout {
+    uint64_t ntiles, nchunks;
+    uint64_t ctl, status, total, off_a, off_b, tok_a, tok_b, bytes, zero_bytes;
+};
+
+WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
+    WsLayout L{};
+    L.ntiles = (n + blt::kTilePos - 1) / blt::kTilePos;
+    L.nchunks = n ? (n + cs - 1) / cs : 0;
+    L.ctl = 0;
+    L.status = blt::kCtlBytes;
+    L.zero_bytes = up16(blt::kCtlBytes + 8 * L.ntiles);
+    L.total = L.zero_bytes;
+    L.off_a = L.total + 16;
+    L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
+    L.tok_a = L.off_b + up16(8 * (L.nchunks + 1));
+    if (single_pass) {
+        L.tok_b = L.tok_a;
+        L.bytes = L.tok_a;
+    } else {
+        L.tok_b = L.tok_a + up16(2 * n);
+        L.bytes = L.tok_b + up16(2 * n);
+    }
+    return L;
+}
+
+int read_u64(const void* dptr, uint64_t* v, hipStream_t s) {
+    HIP_TRY(hipMemcpyAsync(v, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return 0;
+}
+
+int check_ctl(uint8_t* ws, hipStream_t s) {
+    uint32_t ctl[16] = {0};
+    HIP_TRY(hipMemcpyAsync(ctl, ws, sizeof ctl, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ctl[1])
+        return fail(BLT_E_IO,
+                    "merge-scan device check failed (flags 0x%x: 1 look-back timeout, 2 output range, 4 prefix "
+                    "invariant; first at tile %u sub-tile %u, O=%llu, value=%llu, C=%u)",
+                    ctl[1], ctl[2] ? ctl[2] - 1 : 0, ctl[3], (unsigned long long)ctl[4] | ((unsigned long long)ctl[5] << 32),
+                    (unsigned long long)ctl[6] | ((unsigned long long)ctl[7] << 32), ctl[8]);
+    return 0;
+}
+
+// Enqueues one merge pass over n positions.
+int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
+             const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
+             uint64_t out_cap, uint64_t* chunk_off) {
+    const uint64_t ntiles = (n + blt::kTilePos - 1) / blt::kTilePos;
+    if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
+    HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
+    blt::PassParams p{};
+    p.in = in;
+    p.n = n;
+    p.cs = cs;
+    p.cstart = cstart;
+    p.nchunks = L.nchunks;
+    p.out = out;
+    p.out_cap = out_cap;
+    p.chunk_off = chunk_off;
+    p.status = reinterpret_cast<uint64_t*>(ws + L.status);
+    p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
+    p.total = reinterpret_cast<uint64_t*>(ws + L.total);
+    p.ntiles = (uint32_t)ntiles;
+    p.sentinel = h->sentinel;
+    p.dense = t->dense;
+    p.hslots = t->hslots;
+    p.hmask = h->hmask;
+    p.debug = g_debug_tiles;
+    HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
+    return 0;
+}
+
+int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
+                  uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, hipStream_t s, uint64_t* out_tokens) {
+    if (!h || (!d_in && n) || (!d_out && n)) return fail(BLT_E_INVALID_INPUT, "null argument");
+    if (cs == 0) return fail(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
+    if (((uintptr_t)d_in | (uintptr_t)d_out | (uintptr_t)d_ws) & 15)
+        return fail(BLT_E_INVALID_INPUT, "device buffers must be 16-byte aligned");
+    if (n == 0) {
+        if (out_tokens) *out_tokens = 0;
+        if (d_chunk_off) HIP_TRY(hipMemsetAsync(d_chunk_off, 0, sizeof(uint64_t), s));
+        return 0;
+    }
+    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    if (ws_bytes < L.bytes) return fail(BLT_E_INVALID_INPUT, "workspace too small (%zu < %llu)", ws_bytes, (unsigned long long)L.bytes);
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    DevTables* t;
+    if (int rc = device_tables(h, dev, &t)) return rc;
+    uint8_t* ws = static_cast<uint8_t*>(d_ws);
+
+    if (h->single_pass) {
+        if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, d_chunk_off)) return rc;
+        if (out_tokens) {
+            if (int rc = read_u64(ws + L.total, out_tokens, s)) return rc;
+            return check_ctl(ws, s);
+        }
+        return 0;
+    }
+
+    // General map: pass 1 on bytes, then passes on u16 tokens until one merges nothing
+    // (tokenizer.rs:63-86), then big-endian serialisation (:88-91).
+    uint16_t* tok[2] = {reinterpret_cast<uint16_t*>(ws + L.tok_a), reinterpret_cast<uint16_t*>(ws + L.tok_b)};
+    uint64_t* off[2] = {reinterpret_cast<uint64_t*>(ws + L.off_a), reinterpret_cast<uint64_t*>(ws + L.off_b)};
+    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, tok[0], false, 2 * n, off[0])) return rc;
+    uint64_t cur_n;
+    if (int rc = read_u64(ws + L.total, &cur_n, s)) return rc;
+    if (int rc = check_ctl(ws, s)) return rc;
+    int cur = 0;
+    if (cur_n != n) {
+        for (;;) {
+            const int nx = cur ^ 1;
+            if (int rc = run_pass(h, t, dev, s, ws, L, tok[cur], true, cur_n, 0, off[cur], tok[nx], false, 2 * n, off[nx]))
+                return rc;
+            uint64_t nn;
+            if (int rc = read_u64(ws + L.total, &nn, s)) return rc;
+            if (int rc = check_ctl(ws, s)) return rc;
+            if (nn == cur_n) break;  // no merge: output == input
+            cur = nx;
+            cur_n = nn;
+        }
+    }
+    HIP_TRY(blt::launch_bswap16(tok[cur], cur_n, d_out, s));
+    if (d_chunk_off)
+        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+    if (out_tokens) {
+        HIP_TRY(hipStreamSynchronize(s));
+        *out_tokens = cur_n;
+    }
+    return 0;
+}
+
+// ---- per-device staging contexts for the host-buffer API ---------------------------------
+struct DevCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+    uint8_t* d_ws = nullptr;
+    size_t ws_cap = 0;
+    uint64_t* d_off = nullptr;
+    size_t off_cap = 0;
+};
+
+std::mutex g_pool_mu;
+std::vector<DevCtx*> g_pool;  // idle contexts; never freed (process lifetime)
+
+DevCtx* ctx_acquire(int dev) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (g_pool[i]->device == dev) {
+                DevCtx* c = g_pool[i];
+                g_pool.erase(g_pool.begin() + (long)i);
+                return c;
+            }
+    }
+    DevCtx* c = new DevCtx();
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void ctx_release(DevCtx* c) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    g_pool.push_back(c);
+}
+
+int grow(uint8_t** p, size_t* cap, size_t need) {
+    if (*cap >= need && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t sz = std::max<size_t>(need, 4096);
+    HIP_TRY(hipMalloc(p, sz));
+    *cap = sz;
+    return 0;
+}
+
+struct CtxGuard {
+    DevCtx* c;
+    ~CtxGuard() { if (c) ctx_release(c); }
+};
+
+// Encodes host bytes [in, in + n) (chunk size cs) on device dev into host out; returns
+// tokens and optional per-chunk token offsets (nchunks + 1).
+int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uint64_t cs, uint8_t* out,
+                   uint64_t* tokens, std::vector<uint64_t>* chunk_off) {
+    HIP_TRY(hipSetDevice(dev));
+    DevCtx* c = ctx_acquire(dev);
+    if (!c) return fail(BLT_E_IO, "cannot create a HIP stream on device %d", dev);
+    CtxGuard guard{c};
+    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    if (int rc = grow(&c->d_in, &c->in_cap, up16(n))) return rc;
+    if (int rc = grow(&c->d_out, &c->out_cap, up16(2 * n))) return rc;
+    if (int rc = grow(&c->d_ws, &c->ws_cap, L.bytes)) return rc;
+    uint8_t* offp = reinterpret_cast<uint8_t*>(c->d_off);
+    if (int rc = grow(&offp, &c->off_cap, 8 * (L.nchunks + 1))) return rc;
+    c->d_off = reinterpret_cast<uint64_t*>(offp);
+    HIP_TRY(hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream));
+    uint64_t ntok = 0;
+    if (int rc = encode_device(h, c->d_in, n, cs, c->d_out, c->d_off, c->d_ws, c->ws_cap, c->stream, &ntok)) return rc;
+    HIP_TRY(hipMemcpyAsync(out, c->d_out, 2 * ntok, hipMemcpyDeviceToHost, c->stream));
+    if (chunk_off) {
+        chunk_off->resize(L.nchunks + 1);
+        HIP_TRY(hipMemcpyAsync(chunk_off->data(), c->d_off, 8 * (L.nchunks + 1), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *tokens = ntok;
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================================
+// C ABI
+// ===========================================================================================
+extern "C" {
+
+const char* blt_version(void) { return "blt-mi355x 0.1.0"; }
+
+const char* blt_last_error(void) { return t_err.c_str(); }
+
+int blt_load_bpe_merges(const char* path, uint16_t* a, uint16_t* b, uint16_t* v, size_t cap, size_t* n_out) {
+    if (!path || !n_out) return fail(BLT_E_INVALID_INPUT, "null argument");
+    *n_out = 0;
+    std::vector<int32_t> table;
+    if (int rc = load_merges_table(path, table)) return rc;
+    size_t n = 0;
+    for (int i = 0; i < 65536; ++i) n += table[i] >= 0;
+    *n_out = n;
+    if (n > cap) return fail(BLT_E_NOSPC, "need room for %zu entries", n);
+    size_t j = 0;
+    for (int i = 0; i < 65536; ++i)
+        if (table[i] >= 0) {
+            a[j] = (uint16_t)(i >> 8);
+            b[j] = (uint16_t)(i & 255);
+            v[j] = (uint16_t)table[i];
+            ++j;
+        }
+    return 0;
+}
+
+int blt_parse_chunk_size(const char* str, uint64_t* out) {
+    if (!str || !out) return fail(BLT_E_INVALID_INPUT, "null argument");
+    // trim (Unicode White_Space, both ends)
+    std::string s(str);
+    const auto* p = reinterpret_cast<const unsigned char*>(s.data());
+    size_t lo = 0, hi = s.size();
+    while (lo < hi) {
+        uint32_t cp;
+        size_t l = utf8_seq(p + lo, hi - lo, &cp);
+        if (!l || !is_white_space(cp)) break;
+        lo += l;
+    }
+    while (hi > lo) {
+        size_t j = hi - 1;
+        while (j > lo && (p[j] & 0xC0) == 0x80) --j;
+        uint32_t cp;
+        size_t l = utf8_seq(p + j, hi - j, &cp);
+        if (!l || l != hi - j || !is_white_space(cp)) break;
+        hi = j;
+    }
+    const std::string t = s.substr(lo, hi - lo);
+    if (t.empty()) return fail(BLT_E_INVALID_INPUT, "Input string is empty");
+    auto up = [](char c) { return (char)(c >= 'a' && c <= 'z' ? c - 32 : c); };
+    const size_t n = t.size();
+    const bool unit = n >= 2 && (up(t[n - 2]) == 'K' || up(t[n - 2]) == 'M') && up(t[n - 1]) == 'B';
+    const bool digits = std::all_of(t.begin(), t.end(), [](char c) { return c >= '0' && c <= '9'; });
+    std::string num;
+    uint64_t mult = 1;
+    if (unit) {
+        num = t.substr(0, n - 2);
+        mult = up(t[n - 2]) == 'K' ? 1024ull : 1024ull * 1024ull;
+        if (num.empty()) return fail(BLT_E_INVALID_INPUT, "Number part missing for unit '%s'", t.substr(n - 2).c_str());
+    } else if (digits) {
+        num = t;
+    } else {
+        return fail(BLT_E_INVALID_INPUT,
+                    "Invalid unit or format: '%s'. Number must be followed by KB, MB, or be raw bytes.", t.c_str());
+    }
+    uint64_t v = 0;
+    if (*parse_unsigned(num, UINT64_MAX, &v)) return fail(BLT_E_INVALID_INPUT, "Invalid number: '%s'", num.c_str());
+    *out = v * mult;  // release-build wrapping multiply
+    return 0;
+}
+
+uint64_t blt_effective_chunk_size(int has_cli, uint64_t cli, uint64_t threads, uint32_t memcap) {
+    const uint64_t amin = 256ull * 1024, amax = 128ull * 1024 * 1024;
+    const uint64_t dmin = 1024ull * 1024, dmax = 16ull * 1024 * 1024;
+    if (has_cli) return std::min(std::max(cli, amin), amax);
+    const uint64_t usable = (uint64_t)((double)total_ram_bytes() * ((double)memcap / 100.0));
+    uint64_t c = usable / std::max<uint64_t>(threads, 1) / 4;
+    c = std::min(std::max(c, dmin), dmax);
+    return std::min(std::max(c, amin), amax);
+}
+
+uint64_t blt_determine_thread_count(int has_cli, uint64_t threads) {
+    if (has_cli) return threads == 0 ? 1 : threads;
+    const long c = sysconf(_SC_NPROCESSORS_ONLN);
+    return c > 0 ? (uint64_t)c : 1;
+}
+
+int blt_bpe_create(const uint16_t* a, const uint16_t* b, const uint16_t* v, size_t n, uint32_t flags,
+                   blt_bpe** out) {
+    if (!out || (n && (!a || !b || !v))) return fail(BLT_E_INVALID_INPUT, "null argument");
+    if (flags) return fail(BLT_E_INVALID_INPUT, "unknown flags 0x%x", flags);
+    std::vector<uint32_t> keys(n);
+    std::vector<uint16_t> vals(v, v + n);
+    for (size_t i = 0; i < n; ++i) keys[i] = ((uint32_t)a[i] << 16) | b[i];
+    return build_handle(keys, vals, out);
+}
+
+int blt_bpe_create_from_file(const char* path, blt_bpe** out) {
+    if (!path || !out) return fail(BLT_E_INVALID_INPUT, "null argument");
+    std::vector<int32_t> table;
+    if (int rc = load_merges_table(path, table)) {
+        // CoreConfig::load_merges_from_file wraps the loader error (lib.rs:194-201)
+        const std::string inner = t_err;
+        return fail(rc, "Failed to load BPE merges: %s", inner.c_str());
+    }
+    std::vector<uint32_t> keys;
+    std::vector<uint16_t> vals;
+    for (uint32_t i = 0; i < 65536; ++i)
+        if (table[i] >= 0) { keys.push_back(((i >> 8) << 16) | (i & 255)); vals.push_back((uint16_t)table[i]); }
+    return build_handle(keys, vals, out);
+}
+
+void blt_bpe_destroy(blt_bpe* h) {
+    if (!h) return;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);
+        if (h->dev[d].hslots) (void)hipFree(h->dev[d].hslots);
+    }
+    delete h;
+}
+
+int blt_bpe_info(const blt_bpe* h, size_t* n_entries, int* single_pass) {
+    if (!h) return fail(BLT_E_INVALID_INPUT, "null handle");
+    if (n_entries) *n_entries = h->n_entries;
+    if (single_pass) *single_pass = h->single_pass ? 1 : 0;
+    return 0;
+}
+
+size_t blt_bpe_workspace_size(const blt_bpe* h, uint64_t n, uint64_t cs) {
+    if (!h || cs == 0) return 0;
+    return (size_t)ws_layout(h->single_pass, n, cs).bytes;
+}
+
+int blt_bpe_encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
+                          uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, void* stream, uint64_t* out_tokens) {
+    return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens);
+}
+
+int blt_bpe_check_workspace(void* d_ws, void* stream) {
+    if (!d_ws) return fail(BLT_E_INVALID_INPUT, "null workspace");
+    hipStream_t s = (hipStream_t)stream;
+    if (int rc = check_ctl(static_cast<uint8_t*>(d_ws), s)) {
+        uint32_t z[16] = {0};
+        (void)hipMemcpyAsync(d_ws, z, sizeof z, hipMemcpyHostToDevice, s);
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    return 0;
+}
+
+// Not in the public header: a test hook that makes every merge pass record, per tile, its
+// carry-in/offset/look-back lane and both hypothesis counts into a device buffer.
+void blt_debug_set_tile_record(uint64_t* d_buf) { g_debug_tiles = d_buf; }
+
+int blt_basic_encode_device(const uint8_t* d_in, uint64_t n, uint8_t* d_out, void* stream) {
+    if ((!d_in || !d_out) && n) return fail(BLT_E_INVALID_INPUT, "null argument");
+    if (((uintptr_t)d_in | (uintptr_t)d_out) & 15) return fail(BLT_E_INVALID_INPUT, "device buffers must be 16-byte aligned");
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    HIP_TRY(blt::launch_basic_expand(d_in, n, d_out, (hipStream_t)stream));
+    return 0;
+}
+
+int blt_bpe_process_chunk(const blt_bpe* h, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap,
+                          size_t* out_len) {
+    if (!h || !out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return 0;  // tokenizer.rs:57-59
+    if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    uint64_t ntok = 0;
+    if (int rc = encode_host_on(h, dev, in, n, n, out, &ntok, nullptr)) return rc;
+    *out_len = 2 * ntok;
+    return 0;
+}
+
+int blt_basic_process_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, size_t* out_len) {
+    if (!out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
+    *out_len = 0;
+    if (n == 0) return 0;  // tokenizer.rs:109-111
+    if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    DevCtx* c = ctx_acquire(dev);
+    if (!c) return fail(BLT_E_IO, "cannot create a HIP stream");
+    CtxGuard guard{c};
+    if (int rc = grow(&c->d_in, &c->in_cap, up16(n))) return rc;
+    if (int rc = grow(&c->d_out, &c->out_cap, up16(2 * n))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_in, in, n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(blt::launch_basic_expand(c->d_in, n, c->d_out, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, c->d_out, 2 * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *out_len = 2 * n;
+    return 0;
+}
+
+int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t cs, int n_gpus, uint8_t* out,
+                           size_t out_cap, size_t* out_len, uint64_t* chunk_out_len) {
+    if (!h || !out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
+    if (cs == 0) return fail(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
+    *out_len = 0;
+    if (n == 0) return 0;
+    if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return fail(BLT_E_NODEV, "no HIP device available");
+    const uint64_t nchunks = (n + cs - 1) / cs;
+    uint64_t g = (uint64_t)std::max(1, std::min(n_gpus < 1 ? 1 : n_gpus, std::min(count, kMaxDevices)));
+    g = std::min<uint64_t>(g, nchunks);
+    // contiguous chunk ranges, balanced by chunk count (all chunks but the last are full)
+    std::vector<uint64_t> c_lo(g + 1);
+    for (uint64_t r = 0; r <= g; ++r) c_lo[r] = nchunks * r / g;
+    std::vector<uint64_t> tokens(g, 0);
+    std::vector<std::vector<uint64_t>> offs(g);
+    std::vector<int> rcs(g, 0);
+    std::vector<std::string> errs(g);
+    // Each shard is written to its worst-case slot 2 * (first byte) of out, then packed.
+    auto work = [&](uint64_t r) {
+        const uint64_t b0 = c_lo[r] * cs, b1 = std::min<uint64_t>(c_lo[r + 1] * cs, n);
+        rcs[r] = encode_host_on(h, (int)r, in + b0, b1 - b0, cs, out + 2 * b0, &tokens[r], &offs[r]);
+        if (rcs[r]) errs[r] = t_err;
+    };
+    if (g == 1) {
+        int dev;
+        if (int rc = current_device(&dev)) return rc;
+        const int rc = encode_host_on(h, dev, in, n, cs, out, &tokens[0], &offs[0]);
+        if (rc) return rc;
+    } else {
+        std::vector<std::thread> th;
+        for (uint64_t r = 0; r < g; ++r) th.emplace_back(work, r);
+        for (auto& t : th) t.join();
+        for (uint64_t r = 0; r < g; ++r)
+            if (rcs[r]) return fail(rcs[r], "device %llu: %s", (unsigned long long)r, errs[r].c_str());
+        // ordered stitch (pipeline.rs:153-168): shards are in chunk order; close the gaps
+        uint64_t o = 2 * tokens[0];
+        for (uint64_t r = 1; r < g; ++r) {
+            memmove(out + o, out + 2 * c_lo[r] * cs, 2 * tokens[r]);
+            o += 2 * tokens[r];
+        }
+    }
+    uint64_t total = 0;
+    for (uint64_t r = 0; r < g; ++r) {
+        if (chunk_out_len)
+            for (uint64_t k = c_lo[r]; k < c_lo[r + 1]; ++k)
+                chunk_out_len[k] = 2 * (offs[r][k - c_lo[r] + 1] - offs[r][k - c_lo[r]]);
+        total += tokens[r];
+    }
+    *out_len = 2 * total;
+    return 0;
+}
+
+}  // extern "C"

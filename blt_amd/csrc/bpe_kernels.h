@@ -1,0 +1,46 @@
+// Internal interface between the host library (blt_host.cpp) and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace blt {
+
+constexpr int kSub = 4;                       // sub-tiles per look-back tile
+constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
+constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
+
+// Parameters of one merge pass over a whole buffer of positions.
+struct PassParams {
+    const void* in;            // uint8_t bytes (pass 1) or uint16_t tokens (later passes)
+    uint64_t n;                // number of positions
+    uint64_t cs;               // chunk size in positions (pass 1), or 0 to use cstart
+    const uint64_t* cstart;    // cs == 0: chunk start positions [0, nchunks)
+    uint64_t nchunks;
+    void* out;                 // big-endian u16 bytes, or native u16 tokens
+    uint64_t* chunk_off;       // optional [nchunks + 1]: output token index of each chunk start
+    uint64_t* status;          // [ntiles] look-back status words, zeroed before the launch
+    uint32_t* ctl;             // [0] tile ticket, [1] error flags, [2..15] first-error record; zeroed
+    uint64_t out_cap;          // bytes writable at out
+    uint64_t* total;           // number of output tokens
+    uint32_t ntiles;
+    uint32_t sentinel;         // dense table: "absent" value; > 0xFFFF = every byte pair present
+    const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout)
+    const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
+    uint64_t hmask;
+    uint64_t* debug;           // optional [ntiles * 4] per-tile record (tests only)
+};
+
+hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);
+hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s);
+
+// Dense-table layout shared with the host: entry for byte pair (a, b).
+inline uint32_t dense_index(uint32_t a, uint32_t b) { return (a << 8) | (b ^ ((a * 0x35u) & 0xFFu)); }
+
+// Hash used by the general-map slots (must match hash_get in bpe_kernels.hip).
+inline uint64_t slot_hash(uint32_t key) {
+    uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 29);
+}
+
+}  // namespace blt

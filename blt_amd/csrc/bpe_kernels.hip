@@ -1,0 +1,579 @@
+// MI355X (gfx950, CDNA4) kernels for the BPE merge scan of jtrefon/blt.
+//
+// The reference (blt_core/src/tokenizer.rs:56-93) runs, per chunk, greedy left-to-right
+// passes: at position i, if (t[i], t[i+1]) is in the merge map it emits the mapped token and
+// skips 2, otherwise it emits t[i] and skips 1; passes repeat until one merges nothing; tokens
+// are serialised big-endian u16.  Chunks are fixed-size slices of the input and never merge
+// across a boundary (pipeline.rs:73-81), outputs are concatenated in chunk order
+// (pipeline.rs:153-192).
+//
+// One pass is a scan.  Let m[i] = "(t[i], t[i+1]) is a merge and i is not the last position of
+// its chunk", and L[i] = "the scan pointer lands on i".  Then L[0] = 1 and
+// L[i+1] = !(L[i] && m[i]): a chunk start lands automatically because m is 0 at the position
+// before it.  Position i emits iff L[i], emitting map[t[i], t[i+1]] when m[i] and t[i] otherwise;
+// its output index is the number of landings before it.  Merges sit at even offsets of every
+// run of 1s in m that starts on a landing, so a lane turns its 16-position mask into merge and
+// landing masks with three integer ops (merges_for).  A segment's carry function is identity
+// when all 16 positions merge and a constant otherwise, so carries resolve across a wave with
+// two ballots and across the tile with the same trick on the per-wave summaries.
+//
+// Whole-buffer structure: one launch covers every chunk of the buffer.  The buffer is cut into
+// super-tiles of kTilePos positions; a workgroup takes tiles from an atomic ticket (dynamic, so
+// no residency assumption is needed for progress), computes the tile's carry/count function,
+// publishes it, then resolves its carry-in and output offset by a decoupled look-back over
+// 64-bit status words (Merrill & Garland single-pass scan) and writes its compacted tokens,
+// staged through LDS, with 16-byte coalesced stores.  HBM traffic is one read of the input and
+// one write of the output.
+//
+// Byte-pair map (every map loaded from a merges file): the 64K-entry u16 value table lives in
+// LDS (128 KiB of the CU's 160 KiB), XOR-swizzled so English-text lookups spread over the 32
+// banks.  General u16 maps (chained merges, byte-valued merges, u16 wrap) run extra passes on
+// u16 tokens with an open-addressing table in global memory.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bpe_kernels.h"
+
+namespace blt {
+
+constexpr int kThreads = 512;                 // 8 waves; 1 workgroup per CU (LDS-bound)
+constexpr int kWaves = kThreads / 64;
+constexpr int kSeg = 16;                      // positions per lane per sub-tile
+constexpr int kSubPos = kThreads * kSeg;      // 8192 positions per sub-tile
+constexpr int kGroups = kSub * kWaves;        // (sub-tile, wave) groups per tile
+constexpr int kStageBytes = 2 * kSubPos + 32;
+constexpr uint32_t kSpinLimit = 1u << 20;
+static_assert(kTilePos == kSub * kSubPos, "tile geometry");
+
+__device__ __forceinline__ uint32_t swz_index(uint32_t a, uint32_t b) {
+    return (a << 8) | (b ^ ((a * 0x35u) & 0xFFu));
+}
+
+// Merge positions of a 16-position segment whose first position lands iff c.
+__device__ __forceinline__ uint32_t merges_for(uint32_t m, uint32_t c) {
+    uint32_t mc = c ? m : (m & ~1u);           // c = 0: position 0 was consumed by the previous merge
+    uint32_t s = mc & ~(mc << 1);              // run starts
+    uint32_t rodd = mc & ~(mc + (s & 0xAAAAu)); // runs that start at an odd position
+    return (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+}
+
+__device__ __forceinline__ uint32_t lands_for(uint32_t merges, uint32_t c, uint32_t valid) {
+    return ~((merges << 1) | (c ^ 1u)) & valid & 0xFFFFu;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+// Given per-lane {identity?, const carry-out} and counts under carry-in 0/1, resolves each
+// lane's carry-in under both hypotheses for the first lane's carry-in.  Returns the packed
+// (cnt|carry-in=0) | (cnt|carry-in=1) << 16 inclusive prefix; fills lane carry info and the
+// wave's function.
+struct WaveFn {
+    uint32_t ident, cout;   // identity function, or constant carry-out
+    uint32_t cnt0, cnt1;    // total count for carry-in 0 / 1
+};
+
+__device__ __forceinline__ void resolve_wave(uint32_t ident, uint32_t cout, uint32_t cnt0, uint32_t cnt1,
+                                             int lane, uint32_t& has_below, uint32_t& below_cout,
+                                             uint32_t& excl, WaveFn& fn) {
+    uint64_t nonid = __ballot(!ident);
+    uint64_t cmask = __ballot(cout);
+    uint64_t below = nonid & ((1ull << lane) - 1ull);
+    has_below = below != 0;
+    below_cout = has_below ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
+    uint32_t c0 = has_below ? below_cout : 0u;
+    uint32_t c1 = has_below ? below_cout : 1u;
+    uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
+    uint32_t incl = wave_incl_scan(packed, lane);
+    excl = incl - packed;
+    uint32_t tot = __shfl(incl, 63, 64);
+    fn.ident = nonid == 0;
+    fn.cout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+    fn.cnt0 = tot & 0xFFFFu;
+    fn.cnt1 = tot >> 16;
+}
+
+// ---- status words of the decoupled look-back (one per tile) -------------------------------
+// bits 63..62: 0 empty, 1 aggregate, 2 inclusive prefix.
+//  aggregate: bit 61 carry-out for carry-in 1, bit 60 for carry-in 0, bits 30..59 count for
+//             carry-in 1, bits 0..29 count for carry-in 0.
+//  inclusive: bit 61 carry into the next tile, bits 0..60 tokens before the next tile.
+__device__ __forceinline__ uint64_t st_agg(uint32_t co0, uint32_t co1, uint32_t c0, uint32_t c1) {
+    return (1ull << 62) | ((uint64_t)co1 << 61) | ((uint64_t)co0 << 60) | ((uint64_t)c1 << 30) | c0;
+}
+__device__ __forceinline__ uint64_t st_incl(uint32_t carry, uint64_t off) {
+    return (2ull << 62) | ((uint64_t)carry << 61) | off;
+}
+__device__ __forceinline__ void st_publish(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t st_read(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// First failure wins: ctl[2] = T + 1, ctl[3] = sub-tile, ctl[4..5] = O, ctl[6..7] = value, ctl[8] = C.
+__device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint32_t j, uint64_t O, uint64_t v,
+                             uint32_t C) {
+    atomicOr(p.ctl + 1, bit);
+    if (atomicCAS(p.ctl + 2, 0u, T + 1u) == 0u) {
+        p.ctl[3] = j;
+        p.ctl[4] = (uint32_t)O; p.ctl[5] = (uint32_t)(O >> 32);
+        p.ctl[6] = (uint32_t)v; p.ctl[7] = (uint32_t)(v >> 32);
+        p.ctl[8] = C;
+    }
+}
+
+// Lane i's 64-bit value from its two halves.  readlane returns int: cast each half to uint32_t
+// before widening, or the low half sign-extends over the flag and carry bits.
+__device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int i) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, i) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, i);
+}
+
+struct Fn64 {  // tile-sequence function: carry-in c -> (carry-out, count)
+    uint32_t co0, co1;
+    uint64_t c0, c1;
+};
+
+// Wave-wide look-back for tile T (all 64 lanes of one wave).  Returns carry-in and the number
+// of tokens before tile T.
+__device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t& O, uint32_t& how) {
+    const int lane = threadIdx.x & 63;
+    Fn64 acc = {0u, 1u, 0ull, 0ull};   // function of tiles (k+1 .. T-1), identity so far
+    int64_t k = (int64_t)T - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        int64_t idx = k - lane;
+        uint64_t s = idx < 0 ? st_incl(1u, 0ull) : st_read(p.status + idx);
+        uint32_t flag = (uint32_t)(s >> 62);
+        uint64_t incl = __ballot(flag == 2u);
+        uint64_t ready = __ballot(flag != 0u);
+        int f = incl ? (int)__ffsll((unsigned long long)incl) - 1 : 64;
+        uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+        if ((ready & need) != need) {
+            if (++spins > kSpinLimit) {
+                if (lane == 0) atomicOr(p.ctl + 1, 1u);
+                C = 1u; O = 0ull;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
+        if (f < 64) {
+            uint64_t sf = readlane_u64(lo, hi, f);
+            uint32_t carry = (uint32_t)(sf >> 61) & 1u;
+            uint64_t off = sf & ((1ull << 61) - 1ull);
+            for (int i = f - 1; i >= 0; --i) {
+                uint64_t si = readlane_u64(lo, hi, i);
+                off += carry ? ((si >> 30) & 0x3FFFFFFFull) : (si & 0x3FFFFFFFull);
+                carry = carry ? (uint32_t)(si >> 61) & 1u : (uint32_t)(si >> 60) & 1u;
+            }
+            off += carry ? acc.c1 : acc.c0;
+            carry = carry ? acc.co1 : acc.co0;
+            C = carry; O = off;
+            how = (uint32_t)f | ((uint32_t)(T - 1 - k) << 8);
+            return;
+        }
+        // no inclusive prefix in the window: fold the 64 aggregates (tiles k-63 .. k) in front of acc
+        Fn64 w = {0u, 1u, 0ull, 0ull};
+        for (int i = 63; i >= 0; --i) {
+            uint64_t si = readlane_u64(lo, hi, i);
+            uint32_t aco0 = (uint32_t)(si >> 60) & 1u, aco1 = (uint32_t)(si >> 61) & 1u;
+            uint64_t ac0 = si & 0x3FFFFFFFull, ac1 = (si >> 30) & 0x3FFFFFFFull;
+            Fn64 nw;
+            nw.c0 = w.c0 + (w.co0 ? ac1 : ac0);
+            nw.c1 = w.c1 + (w.co1 ? ac1 : ac0);
+            nw.co0 = w.co0 ? aco1 : aco0;
+            nw.co1 = w.co1 ? aco1 : aco0;
+            w = nw;
+        }
+        Fn64 na;
+        na.c0 = w.c0 + (w.co0 ? acc.c1 : acc.c0);
+        na.c1 = w.c1 + (w.co1 ? acc.c1 : acc.c0);
+        na.co0 = w.co0 ? acc.co1 : acc.co0;
+        na.co1 = w.co1 ? acc.co1 : acc.co0;
+        acc = na;
+        k -= 64;
+    }
+}
+
+// ---- chunk boundaries ------------------------------------------------------------------
+// First chunk start >= x (x < n), with its chunk index; returns pos >= n when none.
+__device__ __forceinline__ uint64_t first_boundary(const PassParams& p, uint64_t x, uint64_t& kidx) {
+    if (p.cs) {
+        uint64_t k = (x + p.cs - 1) / p.cs;
+        kidx = k;
+        uint64_t pos = k * p.cs;
+        return pos < p.n ? pos : p.n;
+    }
+    uint64_t lo = 0, hi = p.nchunks;  // lower_bound over cstart[0 .. nchunks)
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (p.cstart[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    kidx = lo;
+    return lo < p.nchunks ? p.cstart[lo] : p.n;
+}
+__device__ __forceinline__ uint64_t next_boundary(const PassParams& p, uint64_t kidx) {
+    if (p.cs) { uint64_t pos = (kidx + 1) * p.cs; return pos < p.n ? pos : p.n; }
+    return kidx + 1 < p.nchunks ? p.cstart[kidx + 1] : p.n;
+}
+
+// ---- position loads ---------------------------------------------------------------------
+template <typename InT> struct Seg;
+
+template <> struct Seg<uint8_t> {
+    uint32_t w[4];
+    __device__ __forceinline__ void load(const uint8_t* in, uint64_t pos, uint64_t n) {
+        if (pos + 16 <= n) {
+            uint4 v = *reinterpret_cast<const uint4*>(in + pos);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = 0;
+            for (int k = 0; k < 16; ++k)
+                if (pos + k < n) w[k >> 2] |= (uint32_t)in[pos + k] << (8 * (k & 3));
+        }
+    }
+    __device__ __forceinline__ uint32_t at(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+    static __device__ __forceinline__ uint32_t load1(const uint8_t* in, uint64_t pos) { return in[pos]; }
+};
+
+template <> struct Seg<uint16_t> {
+    uint32_t w[8];
+    __device__ __forceinline__ void load(const uint16_t* in, uint64_t pos, uint64_t n) {
+        if (pos + 16 <= n) {
+            uint4 a = *reinterpret_cast<const uint4*>(in + pos);
+            uint4 b = *reinterpret_cast<const uint4*>(in + pos + 8);
+            w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+            w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = 0;
+            for (int k = 0; k < 16; ++k)
+                if (pos + k < n) w[k >> 1] |= (uint32_t)in[pos + k] << (16 * (k & 1));
+        }
+    }
+    __device__ __forceinline__ uint32_t at(int k) const { return (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; }
+    static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
+};
+
+__device__ __forceinline__ bool hash_get(const PassParams& p, uint32_t a, uint32_t b, uint32_t& v) {
+    uint32_t key = (a << 16) | b;
+    uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
+    h = (h ^ (h >> 29)) & p.hmask;
+    for (;;) {
+        uint64_t s = p.hslots[h];
+        if (!(s >> 63)) return false;
+        if ((uint32_t)s == key) { v = (uint32_t)(s >> 32) & 0xFFFFu; return true; }
+        h = (h + 1) & p.hmask;
+    }
+}
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t t) { return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu); }
+
+// One merge pass over the whole buffer.  InT = uint8_t: byte input, dense LDS table.
+// InT = uint16_t: token input, global hash table.  kBE: write big-endian u16 (final output),
+// else native u16 tokens for the next pass.
+template <typename InT, bool kBE>
+__global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
+    constexpr bool kDense = sizeof(InT) == 1;
+    __shared__ __attribute__((aligned(16))) uint16_t s_tab[kDense ? 65536 : 8];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kStageBytes];
+    __shared__ WaveFn s_wfn[kGroups];
+    __shared__ uint32_t s_gin[kGroups][4];   // carry-in (H=0, H=1), offset (H=0, H=1)
+    __shared__ uint32_t s_tfn[4];            // tile function: co0, co1, cnt0, cnt1
+    __shared__ uint32_t s_ticket;
+    __shared__ uint32_t s_C;
+    __shared__ uint64_t s_O;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const InT* in = reinterpret_cast<const InT*>(p.in);
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+
+    if constexpr (kDense) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.dense);
+        uint4* dst = reinterpret_cast<uint4*>(s_tab);
+        for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
+    }
+
+    for (;;) {
+        if (tid == 0) s_ticket = atomicAdd(p.ctl, 1u);
+        __syncthreads();
+        const uint32_t T = s_ticket;
+        if (T >= p.ntiles) break;
+        const uint64_t tile0 = (uint64_t)T * kTilePos;
+
+        Seg<InT> seg[kSub];
+        uint32_t vals[kSub][8];
+        uint32_t mm[kSub], valid[kSub], hasb[kSub], bco[kSub], excl[kSub];
+
+        // ---- phase 1: lookups and per-lane / per-wave carry functions --------------------
+#pragma unroll
+        for (int j = 0; j < kSub; ++j) {
+            const uint64_t sub0 = tile0 + (uint64_t)j * kSubPos;
+            const uint64_t pos = sub0 + (uint64_t)tid * kSeg;
+            seg[j].load(in, pos, p.n);
+            uint32_t nxt = __shfl_down(seg[j].at(0), 1, 64);
+            if (lane == 63) nxt = (pos + 16 < p.n) ? Seg<InT>::load1(in, pos + 16) : 0u;
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                uint32_t a = seg[j].at(k);
+                uint32_t b = k < 15 ? seg[j].at(k + 1) : nxt;
+                uint32_t v = 0;
+                bool hit;
+                if constexpr (kDense) {
+                    v = s_tab[swz_index(a, b)];
+                    hit = (p.sentinel > 0xFFFFu) || (v != p.sentinel);
+                } else {
+                    hit = hash_get(p, a, b, v);
+                }
+                m |= (uint32_t)hit << k;
+                if (k & 1) vals[j][k >> 1] |= v << 16; else vals[j][k >> 1] = v;
+            }
+            // valid positions and right neighbours inside the buffer
+            const uint32_t vmask = pos >= p.n ? 0u : (p.n - pos >= 16 ? 0xFFFFu : ((1u << (uint32_t)(p.n - pos)) - 1u));
+            m &= (vmask >> 1) | (pos + 16 < p.n ? 0x8000u : 0u);
+            // no merge across a chunk end: clear m at b - 1 for chunk starts b in (sub0, sub0 + kSubPos]
+            {
+                uint64_t kidx;
+                uint64_t b = first_boundary(p, sub0 + 1 < p.n ? sub0 + 1 : p.n, kidx);
+                while (b < p.n && b <= sub0 + kSubPos) {
+                    uint64_t e = b - 1;
+                    if (e >= pos && e < pos + 16) m &= ~(1u << (uint32_t)(e - pos));
+                    b = next_boundary(p, kidx);
+                    ++kidx;
+                }
+            }
+            mm[j] = m;
+            valid[j] = vmask;
+            const uint32_t ident = m == 0xFFFFu;
+            const uint32_t M1 = merges_for(m, 1u), M0 = merges_for(m, 0u);
+            const uint32_t cnt1 = __popc(lands_for(M1, 1u, vmask));
+            const uint32_t cnt0 = __popc(lands_for(M0, 0u, vmask));
+            const uint32_t cout = ((M1 >> 15) & 1u) ^ 1u;
+            WaveFn fn;
+            resolve_wave(ident, cout, cnt0, cnt1, lane, hasb[j], bco[j], excl[j], fn);
+            if (lane == 0) s_wfn[j * kWaves + wave] = fn;
+        }
+        __syncthreads();
+
+        // ---- phase 2: tile function, publish, look-back ----------------------------------
+        if (wave == 0) {
+            uint32_t gi = 0, gco = 0, g0 = 0, g1 = 0;
+            if (lane < kGroups) { WaveFn f = s_wfn[lane]; gi = f.ident; gco = f.cout; g0 = f.cnt0; g1 = f.cnt1; }
+            else { gi = 1; }
+            uint32_t ghb, gbc, gex;
+            WaveFn tf;
+            // group counts fit 16 bits each (<= 1024 per group, <= 32768 per tile)
+            resolve_wave(gi, gco, g0, g1, lane, ghb, gbc, gex, tf);
+            if (lane < kGroups) {
+                s_gin[lane][0] = ghb ? gbc : 0u;
+                s_gin[lane][1] = ghb ? gbc : 1u;
+                s_gin[lane][2] = gex & 0xFFFFu;
+                s_gin[lane][3] = gex >> 16;
+            }
+            const uint32_t co0 = tf.ident ? 0u : tf.cout, co1 = tf.ident ? 1u : tf.cout;
+            uint32_t C; uint64_t O;
+            uint32_t how = 0xFFFFu;
+            if (T == 0) {
+                C = 1u; O = 0ull;
+            } else {
+                if (lane == 0) st_publish(p.status + T, st_agg(co0, co1, tf.cnt0, tf.cnt1));
+                lookback(p, T, C, O, how);
+            }
+            if (lane == 0) {
+                const uint64_t end = O + (C ? tf.cnt1 : tf.cnt0);
+                // invariant: a position emits at most one token
+                if (O > tile0 || end > p.n) {
+                    record_error(p, 4u, T, 0xFFu, O, end, C);
+                    O = 0; C = 1;
+                }
+                st_publish(p.status + T, st_incl(C ? co1 : co0, end));
+                s_C = C; s_O = O;
+                if (p.debug) {
+                    uint64_t* d = p.debug + 4ull * T;
+                    d[0] = O;
+                    d[1] = ((uint64_t)C << 32) | how;
+                    d[2] = ((uint64_t)tf.cnt1 << 32) | tf.cnt0;
+                    d[3] = ((uint64_t)co1 << 32) | co0;
+                }
+                s_tfn[2] = tf.cnt0; s_tfn[3] = tf.cnt1;
+                if (T == p.ntiles - 1) {
+                    *p.total = end;
+                    if (p.chunk_off) p.chunk_off[p.nchunks] = end;
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- phase 3: compact and store, one sub-tile at a time ---------------------------
+        const uint32_t C = s_C;
+        const uint64_t O = s_O;
+        const uint32_t tile_cnt = C ? s_tfn[3] : s_tfn[2];
+#pragma unroll
+        for (int j = 0; j < kSub; ++j) {
+            const uint64_t sub0 = tile0 + (uint64_t)j * kSubPos;
+            const uint64_t pos = sub0 + (uint64_t)tid * kSeg;
+            const int g = j * kWaves + wave;
+            const uint32_t cg = s_gin[g][C];
+            const uint32_t og = s_gin[g][2 + C];
+            const uint32_t c = hasb[j] ? bco[j] : cg;
+            const uint32_t lane_off = og + (cg ? (excl[j] >> 16) : (excl[j] & 0xFFFFu));
+            const uint32_t sub_first = s_gin[j * kWaves][2 + C];
+            const uint32_t sub_end = (j + 1 < kSub) ? s_gin[(j + 1) * kWaves][2 + C] : tile_cnt;
+            const uint64_t gb = 2ull * (O + sub_first), ge = 2ull * (O + sub_end);
+            const uint64_t ab = gb & ~15ull;
+            const uint32_t M = merges_for(mm[j], c);
+            const uint32_t L = lands_for(M, c, valid[j]);
+            uint16_t* st16 = reinterpret_cast<uint16_t*>(s_stage);
+            uint32_t r = (uint32_t)((2ull * (O + lane_off) - ab) >> 1);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if ((L >> k) & 1u) {
+                    uint32_t v = (vals[j][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    uint32_t tok = ((M >> k) & 1u) ? v : seg[j].at(k);
+                    st16[r++] = (uint16_t)(kBE ? bswap16(tok) : tok);
+                }
+            }
+            // token offsets of chunk starts in this segment
+            if (p.chunk_off) {
+                uint64_t kidx;
+                uint64_t b = first_boundary(p, sub0 < p.n ? sub0 : p.n, kidx);
+                while (b < p.n && b < sub0 + kSubPos) {
+                    if (b >= pos && b < pos + 16 && kidx < p.nchunks) {
+                        uint32_t before = __popc(L & ((1u << (uint32_t)(b - pos)) - 1u));
+                        p.chunk_off[kidx] = O + lane_off + before;
+                    }
+                    b = next_boundary(p, kidx);
+                    ++kidx;
+                }
+            }
+            __syncthreads();
+            if (ge > p.out_cap || gb > ge) {
+                if (tid == 0) record_error(p, 2u, T, (uint32_t)j, O, ge, C);
+                __syncthreads();
+                continue;
+            }
+            const uint32_t nblk = (uint32_t)((ge - ab + 15) >> 4);
+            const uint4* st4 = reinterpret_cast<const uint4*>(s_stage);
+            for (uint32_t i = tid; i < nblk; i += kThreads) {
+                const uint64_t B = ab + 16ull * i;
+                if (B >= gb && B + 16 <= ge) {
+                    *reinterpret_cast<uint4*>(out + B) = st4[i];
+                } else {
+                    for (int u = 0; u < 8; ++u) {
+                        const uint64_t bb = B + 2ull * u;
+                        if (bb >= gb && bb < ge) *reinterpret_cast<uint16_t*>(out + bb) = st16[(bb - ab) >> 1];
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).
+__global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                           uint8_t* __restrict__ out) {
+    const uint64_t nvec = n / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        uint4 v = reinterpret_cast<const uint4*>(in)[i];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            o[2 * q] = ((w[q] & 0xFFu) << 8) | ((w[q] & 0xFF00u) << 16);
+            o[2 * q + 1] = ((w[q] >> 8) & 0xFF00u) | (w[q] & 0xFF000000u);
+        }
+        uint4* dst = reinterpret_cast<uint4*>(out) + 2 * i;
+        dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+    for (uint64_t i = nvec * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        out[2 * i] = 0;
+        out[2 * i + 1] = in[i];
+    }
+}
+
+// Native u16 tokens -> big-endian bytes (the last pass of a multi-pass map found no merge).
+__global__ __launch_bounds__(256) void bswap16_kernel(const uint16_t* __restrict__ in, uint64_t n,
+                                                      uint8_t* __restrict__ out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t nvec = n / 8;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+        uint4 v = reinterpret_cast<const uint4*>(in)[i];
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = ((w[q] & 0x00FF00FFu) << 8) | ((w[q] >> 8) & 0x00FF00FFu);
+        reinterpret_cast<uint4*>(out)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    for (uint64_t i = nvec * 8 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        out[2 * i] = (uint8_t)(in[i] >> 8);
+        out[2 * i + 1] = (uint8_t)in[i];
+    }
+}
+
+// ---- launchers ---------------------------------------------------------------------------
+static int grid_for_tiles(uint32_t ntiles, int device, const void* fn) {
+    static int cached_cus[64] = {0};
+    static int cached_occ[64][4] = {{0}};
+    (void)cached_occ;
+    int cus = device < 64 ? cached_cus[device] : 0;
+    if (!cus) {
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (device < 64) cached_cus[device] = cus;
+    }
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kThreads, 0) != hipSuccess || occ < 1) occ = 1;
+    long long g = (long long)cus * occ;
+    if (g > (long long)ntiles) g = ntiles;
+    return (int)(g < 1 ? 1 : g);
+}
+
+hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s) {
+    if (p.ntiles == 0) return hipSuccess;
+    const void* fn;
+    if (!input_u16) fn = big_endian ? (const void*)merge_pass_kernel<uint8_t, true> : (const void*)merge_pass_kernel<uint8_t, false>;
+    else fn = big_endian ? (const void*)merge_pass_kernel<uint16_t, true> : (const void*)merge_pass_kernel<uint16_t, false>;
+    const int grid = grid_for_tiles(p.ntiles, device, fn);
+    if (!input_u16) {
+        if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint8_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
+        else hipLaunchKernelGGL((merge_pass_kernel<uint8_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
+    } else {
+        if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint16_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
+        else hipLaunchKernelGGL((merge_pass_kernel<uint16_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n / 16 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(basic_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n / 8 + 255) / 256;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(bswap16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+}  // namespace blt

@@ -1,0 +1,147 @@
+/*
+ * blt_bpe.h — C ABI of the MI355X-native BPE merge scan (drop-in for jtrefon/blt's BPE path).
+ *
+ * The reference's boundary for this path is the Rust strategy trait
+ *     #[async_trait] pub trait TokenizationStrategy: Send + Sync {
+ *         async fn process_chunk(&self, chunk_data: &[u8]) -> io::Result<Vec<u8>>;
+ *     }                                                  (blt_core/src/tokenizer.rs:21-31)
+ * with BpeStrategy::new(Arc<BpeMerges>) (tokenizer.rs:43-51), BpeMerges =
+ * HashMap<(u16, u16), u16> (lib.rs:75), the merges loader (config_loader.rs:14-46), and the
+ * chunked pipeline that calls process_chunk once per fixed-size chunk and concatenates results
+ * in chunk order (pipeline.rs:73-81, :141-168).  Every entry point below names the reference
+ * item it replaces.  Plain pointers and sizes only; no C++ or torch types cross the boundary.
+ *
+ * Return convention: 0 on success, a negative errno on failure, with a message for the calling
+ * thread in blt_last_error().  A failing HIP call is -EIO.  The library has no CPU fallback:
+ * every tokenising entry point runs on the GPU and fails with -ENODEV when none is present.
+ *
+ * Threading: a blt_bpe handle is immutable after creation (device copies of its tables are
+ * made once per device, internally synchronised), so all calls are reentrant and may run
+ * concurrently from many threads, as the reference's tokio tasks call one Arc'd strategy.
+ */
+#ifndef BLT_BPE_H
+#define BLT_BPE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLT_ABI_VERSION 1
+
+/* Error kinds of the reference's io::Error, as negative errno values. */
+#define BLT_E_NOT_FOUND (-2)      /* -ENOENT:  io::ErrorKind::NotFound                       */
+#define BLT_E_INVALID_DATA (-74)  /* -EBADMSG: io::ErrorKind::InvalidData (merges file)      */
+#define BLT_E_INVALID_INPUT (-22) /* -EINVAL:  io::ErrorKind::InvalidInput / bad argument     */
+#define BLT_E_NOSPC (-28)         /* -ENOSPC:  caller's output buffer too small               */
+#define BLT_E_NOMEM (-12)         /* -ENOMEM                                                 */
+#define BLT_E_IO (-5)             /* -EIO:     HIP runtime failure / other io::Error          */
+#define BLT_E_NODEV (-19)         /* -ENODEV:  no GPU                                        */
+
+/* Content-type tokens written big-endian before the first chunk (lib.rs:93-104, :284-293). */
+#define BLT_CONTENT_TEXT 0xFF01u
+#define BLT_CONTENT_AUDIO 0xFF02u
+#define BLT_CONTENT_BIN 0xFF03u
+#define BLT_CONTENT_VIDEO 0xFF04u
+
+typedef struct blt_bpe blt_bpe;
+
+/* Library version string ("blt-mi355x <semver>"; the reference reports its crate version via
+ * blt_python's version(), blt_python/src/lib.rs:212-215). */
+const char *blt_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *blt_last_error(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Configuration helpers (CPU; they only parse and compute sizes).
+ * ------------------------------------------------------------------------------------- */
+
+/* load_bpe_merges_from_path (config_loader.rs:14-46): reads a merges file into the map's
+ * entries, sorted by (a, b).  Line i (valid, 0-based) maps (u8, u8) to 256 + i with a wrapping
+ * u16 counter; duplicates overwrite; empty and '#'-first lines are skipped; anything but two
+ * whitespace-separated u8 values is BLT_E_INVALID_DATA with the reference's message.  A missing
+ * file is BLT_E_NOT_FOUND.  If cap is too small: BLT_E_NOSPC with *n_out = entries needed. */
+int blt_load_bpe_merges(const char *path, uint16_t *a, uint16_t *b, uint16_t *v, size_t cap, size_t *n_out);
+
+/* parse_chunk_size_str (utils.rs:10-45): "16MB", "256KB", raw digits; KB/MB are 1024-based. */
+int blt_parse_chunk_size(const char *s, uint64_t *out);
+
+/* get_effective_chunk_size (chunking.rs:26-62): has_cli -> clamp(cli, 256 KiB, 128 MiB);
+ * otherwise clamp(RAM * memcap% / threads / 4, 1 MiB, 16 MiB) from /proc/meminfo MemTotal. */
+uint64_t blt_effective_chunk_size(int has_cli, uint64_t cli_chunk_size, uint64_t threads, uint32_t memcap_percent);
+
+/* determine_thread_count (utils.rs:79-97): has_cli -> max(threads, 1); else logical CPUs. */
+uint64_t blt_determine_thread_count(int has_cli, uint64_t threads);
+
+/* ---------------------------------------------------------------------------------------
+ * Strategy handle: BpeStrategy::new(Arc<BpeMerges>) (tokenizer.rs:43-51).
+ * ------------------------------------------------------------------------------------- */
+
+/* Builds the strategy from n map entries (a[i], b[i]) -> v[i]; a later duplicate key
+ * overwrites an earlier one (HashMap collect).  flags must be 0. */
+int blt_bpe_create(const uint16_t *a, const uint16_t *b, const uint16_t *v, size_t n, uint32_t flags,
+                   blt_bpe **out);
+
+/* CoreConfig::load_bpe_data + BpeStrategy::new (lib.rs:184-201, :271-282): loads a merges file
+ * with exactly the semantics of blt_load_bpe_merges and builds the strategy. */
+int blt_bpe_create_from_file(const char *merges_path, blt_bpe **out);
+
+void blt_bpe_destroy(blt_bpe *h);
+
+/* Number of distinct map entries; *single_pass = 1 when one greedy pass is provably the
+ * fixpoint (no map value is a key component: true for every merges file below 65 281 lines). */
+int blt_bpe_info(const blt_bpe *h, size_t *n_entries, int *single_pass);
+
+/* ---------------------------------------------------------------------------------------
+ * Host-buffer entry points (stage through the GPU; results are bit-exact with the reference).
+ * ------------------------------------------------------------------------------------- */
+
+/* TokenizationStrategy::process_chunk for BpeStrategy (tokenizer.rs:56-93): one chunk ->
+ * big-endian u16 tokens.  out_cap must be >= 2 * n.  Empty input -> *out_len = 0. */
+int blt_bpe_process_chunk(const blt_bpe *h, const uint8_t *in, size_t n, uint8_t *out, size_t out_cap,
+                          size_t *out_len);
+
+/* The mmap pipeline for a BPE strategy (pipeline.rs:56-192): split in into chunks of
+ * chunk_size bytes (pipeline.rs:73-81), tokenise each chunk independently, concatenate in chunk
+ * order.  Chunks shard over n_gpus devices (contiguous chunk ranges, no collective); the output
+ * is identical for every n_gpus.  chunk_out_len (nullable) receives each chunk's output bytes.
+ * out_cap >= 2 * n. */
+int blt_bpe_process_chunks(const blt_bpe *h, const uint8_t *in, size_t n, size_t chunk_size, int n_gpus,
+                           uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *chunk_out_len);
+
+/* BasicTokenizationStrategy::process_chunk (tokenizer.rs:103-124): byte b -> [0, b]. */
+int blt_basic_process_chunk(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len);
+
+/* ---------------------------------------------------------------------------------------
+ * Device-resident entry points (inputs already in HBM on the current HIP device).
+ * ------------------------------------------------------------------------------------- */
+
+/* Bytes of scratch workspace blt_bpe_encode_device needs for n input bytes. */
+size_t blt_bpe_workspace_size(const blt_bpe *h, uint64_t n, uint64_t chunk_size);
+
+/* Whole-buffer BPE over chunks of chunk_size bytes, on the current device and the given HIP
+ * stream (NULL = default stream).  d_in: n bytes, 16-byte aligned.  d_out: 2 * n bytes,
+ * 16-byte aligned; receives the stitched big-endian token stream.  d_chunk_off (nullable):
+ * nchunks + 1 u64, the output token index where each chunk starts, [nchunks] = total tokens.
+ * d_workspace: blt_bpe_workspace_size() bytes.  out_tokens (nullable): if given, the call
+ * waits for the stream and returns the number of output tokens; if NULL and the map is
+ * single-pass, the call only enqueues work (no host synchronisation). */
+int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
+                          uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
+                          void *stream, uint64_t *out_tokens);
+
+/* Reads and clears the device error flags a previous async encode left in d_workspace
+ * (waits for the stream).  0 if clean, BLT_E_IO if a look-back timed out. */
+int blt_bpe_check_workspace(void *d_workspace, void *stream);
+
+/* Basic strategy on device: d_out[2i] = 0, d_out[2i + 1] = d_in[i]. */
+int blt_basic_encode_device(const uint8_t *d_in, uint64_t n, uint8_t *d_out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BLT_BPE_H */

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the reference KATs.
+
+Bit-exact everywhere: this is integer/byte work.  Sizes are chosen so the oracle finishes in
+seconds; the full BASELINE sizes are covered in test_gpu_fullsize.py.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import blt_amd
+from blt_amd import synth
+from oracle import oracle as O
+from tests.conftest import merges_dict, tokens_be
+
+pytestmark = pytest.mark.gpu
+
+TILE = 32768  # positions per look-back tile (bpe_kernels.h kTilePos)
+
+
+def _oracle_chunk(merges, data):
+    return O.COracle(merges).process_chunk(bytes(data))
+
+
+def test_strategy_kats(kats):
+    for c in kats["strategy"]:
+        data = c["input"].encode()
+        if c["kind"] == "bpe":
+            got = blt_amd.BpeStrategy.new(merges_dict(c["merges"])).process_chunk(data)
+            assert got == tokens_be(c["tokens"]), c["name"]
+        elif c["kind"] == "basic":
+            assert blt_amd.BasicTokenizationStrategy().process_chunk(data) == bytes(c["bytes"]), c["name"]
+
+
+def test_cli_merges_kat(kats, tmp_path):
+    c = next(c for c in kats["cli"] if "merges_file" in c)
+    path = tmp_path / "merges.txt"
+    path.write_text(c["merges_file"])
+    s = blt_amd.BpeStrategy.from_file(str(path))
+    assert s.process_chunk(c["stdin"].encode()) == tokens_be(c["tokens"])
+    out = s.process_chunks(np.frombuffer(c["stdin"].encode(), np.uint8), 1024)
+    assert bytes(out) == tokens_be(c["tokens"])
+
+
+def _rand_bytepair_map(rng, density, alphabet=256, base=256):
+    keys = set()
+    target = int(density * alphabet * alphabet)
+    while len(keys) < target:
+        keys.add((rng.randrange(alphabet), rng.randrange(alphabet)))
+    return {k: base + i for i, k in enumerate(sorted(keys))}
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 15, 16, 17, 31, 32, 33, 1023, 1024, 1025, 8191, 8192, 8193,
+                               TILE - 1, TILE, TILE + 1, 2 * TILE + 17, 5 * TILE - 3])
+def test_sizes_random_bytes(n):
+    rng = random.Random(n)
+    m = _rand_bytepair_map(rng, 0.3)
+    data = bytes(rng.randrange(256) for _ in range(n))
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+
+
+@pytest.mark.parametrize("density", [0.0, 0.001, 0.05, 0.5, 0.95, 1.0])
+def test_densities(density):
+    rng = random.Random(int(density * 1000) + 7)
+    m = _rand_bytepair_map(rng, density, alphabet=8)
+    data = bytes(rng.randrange(8) for _ in range(3 * TILE + 12345))
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+
+
+@pytest.mark.parametrize("lead", [0, 1, 2, 3, 17])
+@pytest.mark.parametrize("n", [100, TILE + 5, 3 * TILE, 70 * TILE + 3])
+def test_long_merge_runs_cross_tiles(lead, n):
+    """Every pair merges: the lands parity must carry across lanes, waves, sub-tiles and
+    look-back tiles (identity functions all the way), including windows of > 64 tiles."""
+    m = {(97, 97): 300}
+    data = b"x" * lead + b"a" * n
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+
+
+def test_all_pairs_present_sentinel_free():
+    """65 536 byte-pair keys with 65 536 distinct values: no free sentinel value."""
+    m = {(a, b): (a * 256 + b + 1) & 0xFFFF for a in range(256) for b in range(256)}
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 3 * TILE + 77, dtype=np.uint8).tobytes()
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False  # values collide with key components -> multi-pass map
+    assert s.process_chunk(data) == _oracle_chunk(m, data)
+
+
+def test_general_maps_multipass():
+    """Chained merges (tokenizer.rs:204-212), byte-valued merges (:283-291), u16 keys."""
+    rng = random.Random(11)
+    for trial in range(12):
+        alph = rng.choice([3, 4, 6, 16])
+        m = {}
+        for _ in range(rng.randrange(1, 40)):
+            a = rng.randrange(alph + 8) if rng.random() < 0.5 else rng.randrange(alph)
+            b = rng.randrange(alph + 8) if rng.random() < 0.5 else rng.randrange(alph)
+            v = rng.randrange(alph + 8) if rng.random() < 0.3 else 256 + rng.randrange(64)
+            a = a if a < alph else 256 + (a - alph)
+            b = b if b < alph else 256 + (b - alph)
+            m[(a, b)] = v
+        n = rng.choice([1, 5, 100, 5000, 2 * TILE + 9])
+        data = bytes(rng.randrange(alph) for _ in range(n))
+        got = blt_amd.BpeStrategy(m).process_chunk(data)
+        assert got == _oracle_chunk(m, data), (trial, m)
+
+
+def test_chained_map_long():
+    m = {(97, 97): 97}  # "aa" -> "a": log2(n) passes
+    data = b"a" * 100000 + b"b" + b"a" * 3
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+
+
+@pytest.mark.parametrize("cs", [262144, 300001, 1000000, 1 << 20])
+def test_chunked_pipeline_boundaries(cs):
+    """No merge crosses a chunk boundary (pipeline.rs:73-81); order is kept (:153-192)."""
+    n = 3 * cs + cs // 3
+    data = np.frombuffer(b"a" * n, np.uint8)  # every pair merges: boundaries are visible
+    m = {(97, 97): 256}
+    s = blt_amd.BpeStrategy(m)
+    got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
+
+
+def test_chunked_pipeline_text_general_map():
+    text = synth.text(2_500_000, seed=2)
+    m = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258}  # chained + byte-valued
+    s = blt_amd.BpeStrategy(m)
+    for cs in (262144, 777777):
+        got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(m).run(text, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp)
+        assert np.array_equal(lens, elens)
+
+
+def test_text_cfg_merges_small():
+    """cfg2/cfg3 merge construction on a 4 MiB text sample, 1 MiB chunks."""
+    text = synth.text(4 << 20, seed=2)
+    for pairs in (synth.top_pair_merges(text, 256), synth.text_merges_50k(text, seed=3)):
+        m = synth.merges_dict(pairs)
+        got = blt_amd.BpeStrategy(m).process_chunks(text, 1 << 20)
+        exp = O.COracle(m).run(text, 1 << 20, threads=8)
+        assert np.array_equal(got, exp)
+
+
+def test_random_bytes_50k_merges():
+    data = synth.random_bytes(3 << 20, seed=5)
+    pairs = synth.text_merges_50k(synth.text(1 << 20, seed=3), seed=3)
+    m = synth.merges_dict(pairs)
+    got = blt_amd.BpeStrategy(m).process_chunks(data, 1 << 20)
+    exp = O.COracle(m).run(data, 1 << 20, threads=8)
+    assert np.array_equal(got, exp)
+
+
+def test_multi_gpu_sharding_is_identical():
+    """Output is independent of the GPU count (chunks are independent, §8e)."""
+    data = synth.text(5 << 20, seed=4)
+    m = synth.merges_dict(synth.top_pair_merges(data, 256))
+    s = blt_amd.BpeStrategy(m)
+    one = s.process_chunks(data, 262144, n_gpus=1)
+    many = s.process_chunks(data, 262144, n_gpus=8)  # clamps to the devices present
+    assert np.array_equal(one, many)
+
+
+def test_basic_strategy_sizes():
+    rng = np.random.default_rng(1)
+    for n in (1, 15, 16, 17, 4095, 1 << 20, (1 << 20) + 3):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert blt_amd.BasicTokenizationStrategy().process_chunk(data) == O.basic_process_chunk(data)
+
+
+def test_device_api_chunk_offsets():
+    import torch
+    data = synth.text(3 << 20, seed=9)
+    m = synth.merges_dict(synth.top_pair_merges(data, 256))
+    s = blt_amd.BpeStrategy(m)
+    cs = 262144
+    n = data.size
+    nchunks = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(nchunks + 1, dtype=torch.int64, device="cuda")
+    ws_b = s.workspace_size(n, cs)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), ws_b, stream,
+                          d_off.data_ptr(), sync=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert 2 * tok == exp.size
+    assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp)
+    offs = d_off.cpu().numpy()
+    assert offs[-1] == tok
+    assert np.array_equal(np.diff(offs) * 2, elens)
+    # async form, repeated: same bytes, no device error flags
+    for _ in range(3):
+        s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), ws_b, stream, sync=False)
+    s.check_workspace(ws.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp)

@@ -1,0 +1,110 @@
+"""Pins both CPU restatements (pure Python and C) to the reference's own known-answer tests.
+
+The reference (Rust) cannot run in this image, so these KATs — transcribed as data in
+tests/golden/reference_kats.json from blt_core/src/{tokenizer,config_loader,chunking,utils}.rs
+and tests/cli.rs — are what anchor the oracle.
+"""
+import os
+
+import pytest
+
+from oracle import oracle as O
+from tests.conftest import merges_dict, tokens_be
+
+
+def _strategy_cases(kats):
+    return [(c["name"], c) for c in kats["strategy"]]
+
+
+def test_strategy_kats_python(kats):
+    for c in kats["strategy"]:
+        data = c["input"].encode()
+        if c["kind"] == "bpe":
+            got = O.bpe_process_chunk(merges_dict(c["merges"]), data)
+            assert got == tokens_be(c["tokens"]), c["name"]
+        elif c["kind"] == "basic":
+            assert O.basic_process_chunk(data) == bytes(c["bytes"]), c["name"]
+        else:
+            assert O.passthrough_process_chunk(data) == bytes(c["bytes"]), c["name"]
+
+
+def test_strategy_kats_c(kats):
+    for c in kats["strategy"]:
+        data = c["input"].encode()
+        if c["kind"] == "bpe":
+            got = O.COracle(merges_dict(c["merges"])).process_chunk(data)
+            assert got == tokens_be(c["tokens"]), c["name"]
+        elif c["kind"] == "basic":
+            got = bytes(O.COracle(None).run(data, 1 << 20))
+            assert got == bytes(c["bytes"]), c["name"]
+        else:
+            got = bytes(O.COracle(None).run(data, 1 << 20, passthrough=True))
+            assert got == bytes(c["bytes"]), c["name"]
+
+
+@pytest.mark.parametrize("impl", ["python", "c"])
+def test_loader_kats(kats, tmp_path, impl):
+    load = O.load_bpe_merges_from_path if impl == "python" else O.c_load_merges
+    for c in kats["loader"]:
+        if c["file"] is None:
+            path = str(tmp_path / "this_file_should_not_exist.txt")
+        else:
+            path = str(tmp_path / (c["name"] + ".txt"))
+            with open(path, "w") as f:
+                f.write(c["file"])
+        if "error_kind" in c:
+            with pytest.raises(O.MergeLoadError) as ei:
+                load(path)
+            assert ei.value.kind == c["error_kind"], c["name"]
+            if "error_contains" in c:
+                assert c["error_contains"] in str(ei.value), c["name"]
+        else:
+            assert load(path) == merges_dict(c["merges"]), c["name"]
+
+
+def test_chunk_size_kats(kats):
+    for c in kats["chunk_size_cli"]:
+        assert O.get_effective_chunk_size(c["cli"], c["threads"], c["memcap"], 64 << 30) == c["expected"]
+        assert O.c_effective_chunk_size(c["cli"], c["threads"], c["memcap"], 64 << 30) == c["expected"]
+    for c in kats["chunk_size_dynamic_bounds"]:
+        for ram in (1 << 30, 16 << 30, 64 << 30, 2 << 40):
+            for fn in (O.get_effective_chunk_size, O.c_effective_chunk_size):
+                v = fn(None, c["threads"], c["memcap"], ram)
+                assert c["min"] <= v <= c["max"]
+
+
+def test_parse_chunk_size_kats(kats):
+    for c in kats["parse_chunk_size_valid"]:
+        assert O.parse_chunk_size_str(c["s"]) == c["expected"]
+        assert O.c_parse_chunk_size(c["s"]) == c["expected"]
+    for c in kats["parse_chunk_size_invalid"]:
+        with pytest.raises(ValueError):
+            O.parse_chunk_size_str(c["s"])
+        with pytest.raises(ValueError):
+            O.c_parse_chunk_size(c["s"])
+
+
+def test_thread_count_kats(kats):
+    for c in kats["thread_count"]:
+        assert O.determine_thread_count(c["threads"]) == c["expected"]
+
+
+def test_cli_kats_through_pipeline(kats):
+    """tests/cli.rs end-to-end KATs, replayed through the restated pipeline (single chunk)."""
+    for c in kats["cli"]:
+        data = (c.get("stdin") or c.get("file_input")).encode()
+        if "merges_file" in c:
+            merges = {}
+            for i, line in enumerate(l for l in c["merges_file"].splitlines() if l):
+                a, b = line.split()
+                merges[(int(a), int(b))] = 256 + i
+            got = O.run_chunks(data, 1 << 20, merges=merges)
+            assert got == tokens_be(c["tokens"]), c["name"]
+            continue
+        ct = {65281: "text"}.get(c.get("content_token"))
+        got = O.run_chunks(data, 1 << 20, passthrough=c["mode"] == "passthrough", content_type=ct)
+        exp = bytearray()
+        if ct:
+            exp += c["content_token"].to_bytes(2, "big")
+        exp += data if c["mode"] == "passthrough" else O.basic_process_chunk(data)
+        assert got == bytes(exp), c["name"]
