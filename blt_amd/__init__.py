@@ -192,6 +192,15 @@ class BpeStrategy(TokenizationStrategy):
                                                  ctypes.byref(tok) if sync else None))
         return tok.value if sync else None
 
+    def workspace_reset(self, d_workspace: int, n: int, chunk_size: int, stream: int = 0) -> None:
+        _lib.check(self._L.blt_bpe_workspace_reset(self._h, d_workspace, n, chunk_size, stream or None))
+
+    def encode_device_prezeroed(self, d_in: int, n: int, chunk_size: int, d_out: int, d_workspace: int,
+                                workspace_bytes: int, stream: int = 0, d_chunk_off: int = 0) -> None:
+        """Enqueues only the merge-scan kernel (workspace_reset must precede it on the stream)."""
+        _lib.check(self._L.blt_bpe_encode_device_ex(self._h, d_in, n, chunk_size, d_out, d_chunk_off or None,
+                                                    d_workspace, workspace_bytes, stream or None, None, 1))
+
     def check_workspace(self, d_workspace: int, stream: int = 0) -> None:
         _lib.check(self._L.blt_bpe_check_workspace(d_workspace, stream or None))
 

@@ -70,6 +70,9 @@ _SIGNATURES = {
     "blt_bpe_workspace_size": (ctypes.c_size_t, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
     "blt_bpe_encode_device": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp,
                                              ctypes.c_size_t, _vp, _u64p]),
+    "blt_bpe_encode_device_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, _vp, _vp,
+                                                ctypes.c_size_t, _vp, _u64p, ctypes.c_uint32]),
+    "blt_bpe_workspace_reset": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "blt_bpe_check_workspace": (ctypes.c_int, [_vp, _vp]),
     "blt_basic_encode_device": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp]),
 }

@@ -348,10 +348,10 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
 // Enqueues one merge pass over n positions.
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
-             uint64_t out_cap, uint64_t* chunk_off) {
+             uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false) {
     const uint64_t ntiles = (n + blt::kTilePos - 1) / blt::kTilePos;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
-    HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
+    if (!ws_zeroed) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
     blt::PassParams p{};
     p.in = in;
     p.n = n;
@@ -375,7 +375,8 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
 }
 
 int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
-                  uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, hipStream_t s, uint64_t* out_tokens) {
+                  uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, hipStream_t s, uint64_t* out_tokens,
+                  uint32_t flags = 0) {
     if (!h || (!d_in && n) || (!d_out && n)) return fail(BLT_E_INVALID_INPUT, "null argument");
     if (cs == 0) return fail(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
     if (((uintptr_t)d_in | (uintptr_t)d_out | (uintptr_t)d_ws) & 15)
@@ -394,7 +395,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     uint8_t* ws = static_cast<uint8_t*>(d_ws);
 
     if (h->single_pass) {
-        if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, d_chunk_off)) return rc;
+        if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, d_chunk_off,
+                              (flags & BLT_ENCODE_WORKSPACE_ZEROED) != 0))
+            return rc;
         if (out_tokens) {
             if (int rc = read_u64(ws + L.total, out_tokens, s)) return rc;
             return check_ctl(ws, s);
@@ -659,6 +662,20 @@ size_t blt_bpe_workspace_size(const blt_bpe* h, uint64_t n, uint64_t cs) {
 int blt_bpe_encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
                           uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, void* stream, uint64_t* out_tokens) {
     return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens);
+}
+
+int blt_bpe_encode_device_ex(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
+                             uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, void* stream, uint64_t* out_tokens,
+                             uint32_t flags) {
+    if (flags & ~BLT_ENCODE_WORKSPACE_ZEROED) return fail(BLT_E_INVALID_INPUT, "unknown flags 0x%x", flags);
+    return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens, flags);
+}
+
+int blt_bpe_workspace_reset(const blt_bpe* h, void* d_ws, uint64_t n, uint64_t cs, void* stream) {
+    if (!h || !d_ws || cs == 0) return fail(BLT_E_INVALID_INPUT, "bad argument");
+    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    HIP_TRY(hipMemsetAsync(d_ws, 0, L.zero_bytes, (hipStream_t)stream));
+    return 0;
 }
 
 int blt_bpe_check_workspace(void* d_ws, void* stream) {

@@ -133,6 +133,19 @@ int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uin
                           uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
                           void *stream, uint64_t *out_tokens);
 
+/* Flags of blt_bpe_encode_device_ex. */
+#define BLT_ENCODE_WORKSPACE_ZEROED 1u /* caller ran blt_bpe_workspace_reset on this stream since the
+                                          last encode (single-pass maps; ignored otherwise) */
+
+/* As blt_bpe_encode_device, with flags.  With BLT_ENCODE_WORKSPACE_ZEROED the call enqueues only
+ * the merge-scan kernel, so events around it time that kernel alone. */
+int blt_bpe_encode_device_ex(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
+                             uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
+                             void *stream, uint64_t *out_tokens, uint32_t flags);
+
+/* Enqueues the zeroing of the look-back control words an encode of (n, chunk_size) uses. */
+int blt_bpe_workspace_reset(const blt_bpe *h, void *d_workspace, uint64_t n, uint64_t chunk_size, void *stream);
+
 /* Reads and clears the device error flags a previous async encode left in d_workspace
  * (waits for the stream).  0 if clean, BLT_E_IO if a look-back timed out. */
 int blt_bpe_check_workspace(void *d_workspace, void *stream);
