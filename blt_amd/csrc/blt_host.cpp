@@ -192,7 +192,8 @@ constexpr int kMaxDevices = 64;
 struct DevTables {
     std::once_flag once;
     int status = 0;
-    uint16_t* dense = nullptr;
+    uint16_t* dense = nullptr;      // native u16 values
+    uint16_t* dense_be = nullptr;   // byte-swapped values (big-endian byte pass)
     uint64_t* hslots = nullptr;
 };
 
@@ -200,7 +201,9 @@ struct blt_bpe {
     size_t n_entries = 0;
     bool single_pass = true;
     uint32_t sentinel = 0;                 // > 0xFFFF: every byte pair is a merge
+    uint32_t sentinel_be = 0;              // the sentinel in output (big-endian) byte order
     std::vector<uint16_t> dense;           // 65536, swizzled (blt::dense_index)
+    std::vector<uint16_t> dense_be;        // the same with byte-swapped values
     std::vector<uint64_t> hslots;          // general map, empty when single_pass
     uint64_t hmask = 0;
     DevTables dev[kMaxDevices];
@@ -246,6 +249,10 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
         const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
         if (a < 256 && b < 256) h->dense[blt::dense_index(a, b)] = kv.second;
     }
+    auto bswap = [](uint32_t v) { return (uint16_t)(((v & 0xFF) << 8) | ((v >> 8) & 0xFF)); };
+    h->sentinel_be = h->sentinel > 0xFFFF ? h->sentinel : bswap(h->sentinel);
+    h->dense_be.resize(65536);
+    for (int i = 0; i < 65536; ++i) h->dense_be[i] = bswap(h->dense[i]);
     if (!h->single_pass) {
         uint64_t cap = 16;
         while (cap < 2 * (uint64_t)map.size() + 2) cap <<= 1;
@@ -279,7 +286,10 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
         bool ok = hipStreamCreateWithFlags(&us, hipStreamNonBlocking) == hipSuccess &&
                   hipMalloc(&t.dense, 65536 * sizeof(uint16_t)) == hipSuccess &&
                   hipMemcpyAsync(t.dense, h->dense.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice, us) ==
-                      hipSuccess;
+                      hipSuccess &&
+                  hipMalloc(&t.dense_be, 65536 * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.dense_be, h->dense_be.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                                 us) == hipSuccess;
         if (ok && !h->hslots.empty()) {
             const size_t bytes = h->hslots.size() * sizeof(uint64_t);
             ok = hipMalloc(&t.hslots, bytes) == hipSuccess &&
@@ -307,7 +317,8 @@ struct WsLayout {
 
 WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     WsLayout L{};
-    L.ntiles = (n + blt::kTilePos - 1) / blt::kTilePos;
+    const uint64_t tile = std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes);
+    L.ntiles = (n + tile - 1) / tile;
     L.nchunks = n ? (n + cs - 1) / cs : 0;
     L.ctl = 0;
     L.status = blt::kCtlBytes;
@@ -349,7 +360,9 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
              uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false) {
-    const uint64_t ntiles = (n + blt::kTilePos - 1) / blt::kTilePos;
+    const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes;   // the byte-pass fast kernel
+    const uint64_t tile = columnar ? blt::kTilePosBytes : blt::kTilePos;
+    const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
     if (!ws_zeroed) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
     blt::PassParams p{};
@@ -365,12 +378,13 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     p.total = reinterpret_cast<uint64_t*>(ws + L.total);
     p.ntiles = (uint32_t)ntiles;
-    p.sentinel = h->sentinel;
-    p.dense = t->dense;
+    p.sentinel = (columnar && be) ? h->sentinel_be : h->sentinel;
+    p.dense = (columnar && be) ? t->dense_be : t->dense;
     p.hslots = t->hslots;
     p.hmask = h->hmask;
     p.debug = g_debug_tiles;
-    HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
+    if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, dev, s));
+    else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }
 
@@ -642,6 +656,7 @@ void blt_bpe_destroy(blt_bpe* h) {
     if (!h) return;
     for (int d = 0; d < kMaxDevices; ++d) {
         if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);
+        if (h->dev[d].dense_be) (void)hipFree(h->dev[d].dense_be);
         if (h->dev[d].hslots) (void)hipFree(h->dev[d].hslots);
     }
     delete h;

@@ -7,6 +7,8 @@ namespace blt {
 
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
+constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
+constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 
 // Parameters of one merge pass over a whole buffer of positions.
@@ -24,18 +26,23 @@ struct PassParams {
     uint64_t* total;           // number of output tokens
     uint32_t ntiles;
     uint32_t sentinel;         // dense table: "absent" value; > 0xFFFF = every byte pair present
-    const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout)
+    const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout); for a
+                               // big-endian byte pass: values (and sentinel) byte-swapped
     const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
     uint64_t hmask;
-    uint64_t* debug;           // optional [ntiles * 4] per-tile record (tests only)
+    uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
+                               // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime stamps
 };
 
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);
+// Byte-input pass (segment kernel, seg::scan_bytes_kernel): p.cs >= kMinChunkBytes; tiles of
+// kTilePosBytes positions.
+hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Dense-table layout shared with the host: entry for byte pair (a, b).
-inline uint32_t dense_index(uint32_t a, uint32_t b) { return (a << 8) | (b ^ ((a * 0x35u) & 0xFFu)); }
+inline uint32_t dense_index(uint32_t a, uint32_t b) { return (a << 8) | (b ^ ((a << 1) & 0xFEu)); }
 
 // Hash used by the general-map slots (must match hash_get in bpe_kernels.hip).
 inline uint64_t slot_hash(uint32_t key) {

@@ -46,7 +46,7 @@ constexpr uint32_t kSpinLimit = 1u << 20;
 static_assert(kTilePos == kSub * kSubPos, "tile geometry");
 
 __device__ __forceinline__ uint32_t swz_index(uint32_t a, uint32_t b) {
-    return (a << 8) | (b ^ ((a * 0x35u) & 0xFFu));
+    return (a << 8) | (b ^ ((a << 1) & 0xFEu));   // = dense_index (bpe_kernels.h)
 }
 
 // Merge positions of a 16-position segment whose first position lands iff c.
@@ -483,6 +483,347 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
     }
 }
 
+// ===========================================================================================
+// Byte-input pass (the hot path: every map loaded from a merges file).
+//
+// Geometry: a workgroup of kThreads lanes takes a tile of kS sub-tiles; in a sub-tile lane l
+// of wave w owns 16 consecutive positions (one 16-byte load), so a wave owns 1024 contiguous
+// positions and emits them as one contiguous run of tokens.
+//
+// Phase 1 (no synchronisation): per lane, 16 table lookups from LDS, then the 16-bit merge
+// mask is scanned under BOTH carry-in hypotheses at once — carry 0 in the low 16 bits, carry 1
+// in the high 16 bits of one register, with packed 16-bit adds/shifts (see merges_for).  A
+// wave resolves its lanes' carries with two ballots and one packed prefix scan.
+// Phase 2 (one barrier): the kS x kWaves wave functions give the tile function; wave 0
+// publishes it and resolves the tile's carry-in and output offset by the decoupled look-back.
+// Phase 3 (no block barriers): each wave writes its tokens to a private LDS stage — every lane
+// writes one u16 per position in order; a consumed position writes the slot that the next
+// (landing) position then overwrites, since no two consecutive positions are both consumed —
+// and copies the stage out with 16-byte stores.  As a sub-tile's input registers free up they
+// are refilled with the next tile's bytes, so its loads fly while this tile is written.
+// ===========================================================================================
+namespace seg {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_shl1(uint32_t v) {
+    const u16x2 r = __builtin_bit_cast(u16x2, v) << (u16x2){1, 1};            // v_pk_lshlrev_b16
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    const u16x2 r = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);   // v_pk_add_u16
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+constexpr int kThreads = 512;
+constexpr int kWaves = kThreads / 64;
+constexpr int kS = 4;                                  // sub-tiles per tile
+constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
+constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
+constexpr int kGroups = kS * kWaves;
+constexpr int kStageWave = 2 * (int)kWavePos + 32;     // tokens + 16-byte alignment slack
+static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
+static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
+static_assert(kGroups <= 64, "one lane per group in the tile resolve");
+static_assert(kStageWave % 16 == 0, "stage alignment");
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+
+// Buffer resource over in[base, n) (records clamped): out-of-range loads return 0.  Built from
+// wave-uniform values only, so the loads need no waterfall loop (cdna guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* in, uint64_t base, uint64_t n) {
+    const uint64_t left = base < n ? n - base : 0;
+    const uint32_t records = uni((uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left));
+    const uint64_t addr = uni64((uint64_t)(uintptr_t)(in + (base < n ? base : 0)));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uintptr_t)addr), (short)0, (int)records,
+                                             0x00020000);
+}
+
+// A lane's 16 bytes at byte `off` of the resource; the byte after the wave's range for lane 63.
+// Full wave ranges take one 16-byte load; the buffer's last wave range takes checked bytes.
+__device__ __forceinline__ void load_sub(__amdgpu_buffer_rsrc_t r, bool full, int lane, uint32_t (&x)[4],
+                                         uint32_t& nxt) {
+    if (full) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0);
+        x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t d = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                d |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, 16 * lane + 4 * q + b, 0, 0) << (8 * b);
+            x[q] = d;
+        }
+    }
+    nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)kWavePos, 0, 0);
+}
+
+template <bool kBE>
+__global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
+    __shared__ uint32_t s_wfn[kGroups][4];    // ident, cout, cnt|c=0, cnt|c=1
+    __shared__ uint32_t s_gin[kGroups][4];    // carry-in |H=0, |H=1, offset |H=0, |H=1
+    __shared__ uint32_t s_C;
+    __shared__ uint64_t s_O;
+    __shared__ uint32_t s_ticket[2];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wave = uni((uint32_t)tid >> 6);
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+    const uint64_t n = p.n, cs = p.cs;
+    const uint32_t S = p.sentinel;              // table's "absent" (0x10000: every pair merges)
+    const uint32_t ntiles = p.ntiles;
+
+    if (tid == 0) {
+        s_ticket[0] = atomicAdd(p.ctl, 1u);
+        s_ticket[1] = atomicAdd(p.ctl, 1u);
+    }
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(p.dense);
+        uint4* dst = reinterpret_cast<uint4*>(s_tab);
+        for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+    uint32_t T = uni(s_ticket[0]);
+    uint32_t Tn = uni(s_ticket[1]);
+
+    uint32_t x[kS][4];      // input bytes of each sub-tile
+    uint32_t nxt[kS];       // byte after this wave's range (lane 63's right neighbour)
+    if (T < ntiles) {
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+            const uint64_t wb = (uint64_t)T * kTilePosBytes + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+            load_sub(rsrc(in, wb, n), wb + kWavePos <= n, lane, x[j], nxt[j]);
+        }
+    }
+
+    while (T < ntiles) {
+        const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
+        const uint64_t ts0 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t vals[kS][8];   // looked-up values (output byte order), two per register
+        uint32_t mv[kS];        // merge mask | valid mask << 16
+        uint32_t lw[kS];        // bit 0: a non-identity lane below; bit 1: its carry-out
+        uint32_t ex[kS];        // exclusive prefix count, carry-in 0 | carry-in 1 << 16
+
+        // first chunk start > this wave's first position; advanced monotonically below
+        uint64_t bnext = uni64(((tile0 + (uint64_t)wave * kWavePos) / cs + 1) * cs);
+
+        // ---- phase 1: lookups, lane functions, wave functions ---------------------------------
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+            const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+            const uint32_t lo16 = 16u * (uint32_t)lane;
+            while (bnext <= wb) bnext += cs;
+            // positions left in the buffer from this wave's first one (clamped: uniform 32-bit)
+            const uint32_t rem = wb >= n ? 0u : (n - wb > 2u * kWavePos ? 2u * kWavePos : (uint32_t)(n - wb));
+            // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63
+            // keeps the "old" operand, the byte after the wave's range
+            const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt[j], (int)x[j][0], 0x130, 0xF, 0xF,
+                                                                      false) & 0xFFu;
+            uint32_t m = 0;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
+                const uint32_t lo = x[j][h >> 1], hi = (h >> 1) < 3 ? x[j][(h >> 1) + 1] : nb;
+                const uint32_t t0 = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
+                const uint32_t t = t0 ^ ((t0 >> 7) & 0x00FE00FEu);            // bank swizzle of b
+                const uint32_t va = s_tab[t & 0xFFFFu];
+                const uint32_t vb = s_tab[t >> 16];
+                vals[j][h] = va | (vb << 16);
+                m |= ((uint32_t)(va != S) << (2 * h)) | ((uint32_t)(vb != S) << (2 * h + 1));
+            }
+            // valid positions, right neighbours inside the buffer, chunk ends
+            const int32_t r = (int32_t)rem - (int32_t)lo16;                   // positions left from mine
+            const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
+            m &= (vmask >> 1) | (r > 16 ? 0x8000u : 0u);
+            if (bnext < n && bnext - 1 - wb < kWavePos) {                     // chunk end b - 1 here
+                const uint32_t e = (uint32_t)(bnext - 1 - wb) - lo16;
+                if (e < 16u) m &= ~(1u << e);
+            }
+            mv[j] = m | (vmask << 16);
+            // lane function, both carry-in hypotheses: low half c = 0 (position 0 consumed),
+            // high half c = 1 (merges_for, packed 16-bit)
+            const uint32_t mc = (m & ~1u) | (m << 16);
+            const uint32_t st = mc & ~pk_shl1(mc);
+            const uint32_t rodd = mc & ~pk_add(mc, st & 0xAAAAAAAAu);
+            const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
+            const uint32_t L = ~(pk_shl1(M) | 1u) & (vmask | (vmask << 16));
+            const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
+            const uint32_t cout = ((M >> 31) & 1u) ^ 1u;                     // = carry-0 one if not identity
+            const uint32_t ident = m == 0xFFFFu;
+            // wave resolve
+            const uint64_t nonid = __ballot(!ident);
+            const uint64_t cmask = __ballot(cout);
+            const uint64_t below = nonid & ((1ull << lane) - 1ull);
+            const uint32_t hb = below != 0;
+            const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
+            const uint32_t c0 = hb ? bc : 0u, c1 = hb ? bc : 1u;
+            const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
+            const uint32_t incl = wave_incl_scan(packed, lane);
+            ex[j] = incl - packed;
+            lw[j] = hb | (bc << 1);
+            if (lane == 63) {
+                const uint32_t g = (uint32_t)j * kWaves + wave;
+                s_wfn[g][0] = nonid == 0;
+                s_wfn[g][1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+                s_wfn[g][2] = incl & 0xFFFFu;
+                s_wfn[g][3] = incl >> 16;
+            }
+        }
+        __syncthreads();
+        const uint64_t ts1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
+
+        // ---- phase 2: tile function, publish, look-back (wave 0) ------------------------------
+        if (wave == 0) {
+            uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
+            if (lane < kGroups) { gi = s_wfn[lane][0]; gco = s_wfn[lane][1]; g0 = s_wfn[lane][2]; g1 = s_wfn[lane][3]; }
+            const uint64_t nonid = __ballot(!gi);
+            const uint64_t cmask = __ballot(gco);
+            const uint64_t below = nonid & ((1ull << lane) - 1ull);
+            const uint32_t hb = below != 0;
+            const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
+            const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
+            const uint32_t my0 = cin0 ? g1 : g0, my1 = cin1 ? g1 : g0;
+            const uint32_t inc0 = wave_incl_scan(my0, lane), inc1 = wave_incl_scan(my1, lane);
+            if (lane < kGroups) {
+                s_gin[lane][0] = cin0;
+                s_gin[lane][1] = cin1;
+                s_gin[lane][2] = inc0 - my0;
+                s_gin[lane][3] = inc1 - my1;
+            }
+            const uint32_t tot0 = __shfl(inc0, 63, 64), tot1 = __shfl(inc1, 63, 64);
+            const uint32_t tident = nonid == 0;
+            const uint32_t tcout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+            const uint32_t co0 = tident ? 0u : tcout, co1 = tident ? 1u : tcout;
+            uint32_t C;
+            uint64_t O;
+            uint32_t how = 0xFFFFu;
+            if (T == 0) {
+                C = 1u; O = 0ull;
+            } else {
+                if (lane == 0) st_publish(p.status + T, st_agg(co0, co1, tot0, tot1));
+                lookback(p, T, C, O, how);
+            }
+            if (lane == 0) {
+                const uint64_t end = O + (C ? tot1 : tot0);
+                if (O > tile0 || end > n) {
+                    record_error(p, 4u, T, 0xFFu, O, end, C);
+                    O = 0; C = 1;
+                }
+                st_publish(p.status + T, st_incl(C ? co1 : co0, end));
+                s_C = C; s_O = O;
+                if (T == ntiles - 1) {
+                    *p.total = end;
+                    if (p.chunk_off) p.chunk_off[p.nchunks] = end;
+                }
+                if (p.debug) {
+                    uint64_t* d = p.debug + 4ull * T;
+                    d[0] = O;
+                    d[1] = ((uint64_t)C << 32) | how;
+                    d[2] = ((uint64_t)tot1 << 32) | tot0;
+                    d[3] = ((uint64_t)co1 << 32) | co0;
+                }
+            }
+        }
+        if (tid == 64) s_ticket[0] = atomicAdd(p.ctl, 1u);   // the tile after Tn
+        __syncthreads();
+        const uint64_t ts2 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
+
+        // ---- phase 3: emit each sub-tile's tokens; refill registers with tile Tn -------------
+        {
+            const uint32_t C = uni(s_C);
+            const uint64_t O = uni64(s_O);
+            // first chunk start >= this wave's first position; advanced monotonically below
+            uint64_t cnext = uni64(((tile0 + (uint64_t)wave * kWavePos + cs - 1) / cs) * cs);
+            uint8_t* st = s_stage[wave];
+            uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+                const uint32_t g = (uint32_t)j * kWaves + wave;
+                const uint32_t cg = uni(s_gin[g][C]);
+                const uint64_t og = O + uni(s_gin[g][2 + C]);            // wave's first token
+                const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+                const uint32_t m = mv[j] & 0xFFFFu, vmask = mv[j] >> 16;
+                const uint32_t c = (lw[j] & 1u) ? (lw[j] >> 1) : cg;
+                const uint32_t lane_off = cg ? (ex[j] >> 16) : (ex[j] & 0xFFFFu);
+                const uint32_t mc = c ? m : (m & ~1u);
+                const uint32_t sst = mc & ~(mc << 1);
+                const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
+                const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+                const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
+                const uint32_t my_cnt = __popc(L);
+                const uint32_t wcnt = uni((uint32_t)__shfl(lane_off + my_cnt, 63, 64));
+                const uint64_t gb = 2ull * og;
+                const uint64_t ab = gb & ~15ull;
+                // byte address in the stage of this lane's next token
+                uint32_t a = (uint32_t)(gb - ab) + 2u * lane_off;
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    const uint32_t k = 2u * (uint32_t)h;
+                    const uint32_t xw = x[j][h >> 1];
+                    // raw bytes k, k+1 as tokens: BE [0, x] or native [x, 0] per 16-bit half
+                    const uint32_t xp = __builtin_amdgcn_perm(xw, xw, kBE ? ((h & 1) ? 0x030C020Cu : 0x010C000Cu)
+                                                                          : ((h & 1) ? 0x0C030C02u : 0x0C010C00u));
+                    const uint32_t mlo = (uint32_t)__builtin_amdgcn_sbfe((int)M, (int)k, 1);
+                    const uint32_t mhi = (uint32_t)__builtin_amdgcn_sbfe((int)M, (int)k + 1, 1);
+                    const uint32_t msk = __builtin_amdgcn_perm(mhi, mlo, 0x05040100u);
+                    const uint32_t tok = (vals[j][h] & msk) | (xp & ~msk);
+                    st16[a >> 1] = (uint16_t)tok;
+                    a += 2u * ((L >> k) & 1u);
+                    if (h < 7 || ((L >> 15) & 1u)) st16[a >> 1] = (uint16_t)(tok >> 16);
+                    a += 2u * ((L >> (k + 1)) & 1u);
+                }
+                // token index of a chunk start in this lane's segment
+                while (cnext < wb) cnext += cs;
+                if (p.chunk_off && cnext < n && cnext - wb < kWavePos) {
+                    const uint32_t e = (uint32_t)(cnext - wb) - 16u * (uint32_t)lane;
+                    if (e < 16u) p.chunk_off[cnext / cs] = og + lane_off + __popc(L & ((1u << e) - 1u));
+                }
+                // refill this sub-tile's registers with tile Tn (loads fly during the copy-out)
+                if (Tn < ntiles) {
+                    const uint64_t nb2 = (uint64_t)Tn * kTilePosBytes + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+                    load_sub(rsrc(in, nb2, n), nb2 + kWavePos <= n, lane, x[j], nxt[j]);
+                }
+                // stage -> global (this wave wrote the stage: wait for its LDS writes)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint64_t ge = gb + 2ull * wcnt;
+                if (ge > p.out_cap) {
+                    if (lane == 0) record_error(p, 2u, T, g, O, ge, C);
+                } else {
+                    const uint32_t nblk = (uint32_t)((ge - ab + 15) >> 4);
+                    for (uint32_t i = (uint32_t)lane; i < nblk; i += 64) {
+                        const uint64_t B = ab + 16ull * i;
+                        if (B >= gb && B + 16 <= ge) {
+                            *reinterpret_cast<uint4*>(out + B) = *reinterpret_cast<const uint4*>(st + 16 * i);
+                        } else {
+                            for (int u = 0; u < 8; ++u) {
+                                const uint64_t bb = B + 2ull * u;
+                                if (bb >= gb && bb < ge) *reinterpret_cast<uint16_t*>(out + bb) = st16[8 * i + u];
+                            }
+                        }
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+        if (p.debug && tid == 0) {
+            uint64_t* d = p.debug + 4ull * ntiles + 4ull * T;
+            d[0] = ts0; d[1] = ts1; d[2] = ts2; d[3] = __builtin_amdgcn_s_memtime();
+        }
+        T = Tn;
+        Tn = uni(s_ticket[0]);
+        __syncthreads();   // s_ticket / s_gin / s_C / s_wfn reuse in the next iteration
+    }
+}
+
+}  // namespace seg
+
 // Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).
 __global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                            uint8_t* __restrict__ out) {
@@ -555,6 +896,20 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
         if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint16_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
         else hipLaunchKernelGGL((merge_pass_kernel<uint16_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int device, hipStream_t s) {
+    if (p.ntiles == 0) return hipSuccess;
+    const void* fn = big_endian ? (const void*)seg::scan_bytes_kernel<true> : (const void*)seg::scan_bytes_kernel<false>;
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, seg::kThreads, 0) != hipSuccess || occ < 1) occ = 1;
+    long long grid = (long long)(cus > 0 ? cus : 1) * occ;
+    if (grid > (long long)p.ntiles) grid = p.ntiles;
+    if (big_endian) hipLaunchKernelGGL(seg::scan_bytes_kernel<true>, dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
+    else hipLaunchKernelGGL(seg::scan_bytes_kernel<false>, dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
     return hipGetLastError();
 }
 

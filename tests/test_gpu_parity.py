@@ -200,3 +200,32 @@ def test_device_api_chunk_offsets():
     s.check_workspace(ws.data_ptr(), stream)
     torch.cuda.synchronize()
     assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("cs", [4095, 4096, 4097, 6000, 8191, 32768, 32769, 65536 + 7])
+@pytest.mark.parametrize("kind", ["run", "random"])
+def test_columnar_chunk_edges(cs, kind):
+    """Chunk ends at every alignment the byte-pass kernel sees: column (64), wave (2048) and
+    tile (32768) edges, and the smallest chunk size it accepts (4096; 4095 takes the general
+    kernel)."""
+    n = 5 * 32768 + 123
+    if kind == "run":
+        data = np.frombuffer(b"a" * n, np.uint8)
+        m = {(97, 97): 300}
+    else:
+        rng = np.random.default_rng(cs)
+        data = rng.integers(0, 4, n, dtype=np.uint8)
+        m = {(a, b): 256 + 4 * a + b for a in range(4) for b in range(4) if (a + b) % 3}
+    got, lens = blt_amd.BpeStrategy(m).process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("n", [4096, 4097, 32767, 32768, 32769, 2048 * 3 + 63, 2048 * 3 + 64, 2048 * 3 + 65])
+def test_columnar_tails(n):
+    """Buffer ends inside a column, at a wave edge and at a tile edge (hardware-bounded loads)."""
+    rng = np.random.default_rng(n)
+    data = rng.integers(0, 3, n, dtype=np.uint8).tobytes()
+    m = {(0, 1): 256, (1, 1): 257, (2, 0): 258, (1, 2): 259}
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)

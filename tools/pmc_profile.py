@@ -1,0 +1,83 @@
+"""Collects rocprofv3 PMC counters for the merge-scan kernel, one counter group per pass.
+
+    python tools/pmc_profile.py OUTDIR [--groups A,B,...] [-- bench args]
+
+Each group runs `rocprofv3 --pmc <counters> --kernel-trace --output-format csv -- python
+bench.py ...` as a child process (counters in their own passes, never with sys/runtime
+traces), then averages every counter per dispatch of the kernels whose name contains
+--kernel (default scan_bytes_kernel).  Writes OUTDIR/pmc_summary.json, including the HBM
+traffic per launch corrected as MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE counts
+half of a wide streaming read (doubled here), WRITE_SIZE is exact; both are in KiB.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+GROUPS = {
+    "time": ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+             "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA"],
+    "insts": ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+              "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS"],
+    "misc": ["SQ_WAVES", "SQ_INSTS_BRANCH", "SQ_INSTS_SMEM", "SQ_ACTIVE_INST_VMEM", "SQ_INST_CYCLES_VMEM_RD",
+             "SQ_INST_CYCLES_VMEM_WR", "SQ_LDS_UNALIGNED_STALL", "GRBM_GUI_ACTIVE"],
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+}
+
+
+def run_group(outdir, name, counters, bench_args, kernel):
+    d = os.path.join(outdir, name)
+    os.makedirs(d, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+           "--", sys.executable, os.path.join(ROOT, "bench.py"), *bench_args]
+    print("+", " ".join(cmd), flush=True)
+    with open(os.path.join(d, "log.txt"), "w") as log:
+        rc = subprocess.run(cmd, stdout=log, stderr=subprocess.STDOUT, timeout=900).returncode
+    if rc != 0:
+        raise SystemExit(f"rocprofv3 pass {name} failed with {rc} (see {d}/log.txt)")
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    sums, disp = {}, {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if kernel not in row.get("Kernel_Name", ""):
+                    continue
+                cname = row["Counter_Name"]
+                sums[cname] = sums.get(cname, 0.0) + float(row["Counter_Value"])
+                disp.setdefault(cname, set()).add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+    return {k: sums[k] / max(1, len(disp[k])) for k in sums}, {k: len(v) for k, v in disp.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("outdir")
+    ap.add_argument("--groups", default=",".join(GROUPS))
+    ap.add_argument("--kernel", default="scan_bytes_kernel")
+    ap.add_argument("bench_args", nargs=argparse.REMAINDER)
+    a = ap.parse_args()
+    bench_args = [x for x in a.bench_args if x != "--"] or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline"]
+    os.makedirs(a.outdir, exist_ok=True)
+    result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}}
+    for g in a.groups.split(","):
+        vals, nd = run_group(a.outdir, g, GROUPS[g], bench_args, a.kernel)
+        result["per_dispatch"].update(vals)
+        result["dispatches"].update(nd)
+    pd = result["per_dispatch"]
+    if "FETCH_SIZE" in pd and "WRITE_SIZE" in pd:
+        result["hbm_bytes_per_launch"] = int((2.0 * pd["FETCH_SIZE"] + pd["WRITE_SIZE"]) * 1024)
+        result["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 FETCH_SIZE counts half of wide reads"
+    with open(os.path.join(a.outdir, "pmc_summary.json"), "w") as f:
+        json.dump(result, f, indent=1, sort_keys=True)
+    print(json.dumps(result, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

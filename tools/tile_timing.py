@@ -1,0 +1,57 @@
+"""Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook).
+
+    python tools/tile_timing.py [MiB]
+Prints mean/median cycles of phase 1 (lookups + wave functions), phase 2 (tile resolve +
+look-back), phase 3 (emission + copy-out) and the look-back window statistics."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import blt_amd  # noqa: E402
+from blt_amd import synth  # noqa: E402
+
+TILE = 32768
+CHUNK = 16 << 20
+
+
+def main():
+    mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    n = mib << 20
+    merges = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
+    s = blt_amd.BpeStrategy(merges)
+    d_in = torch.from_numpy(synth.text(n, seed=3)).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    wsb = s.workspace_size(n, CHUNK)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    ntiles = (n + TILE - 1) // TILE
+    dbg = torch.zeros(8 * ntiles, dtype=torch.int64, device="cuda")
+    L = blt_amd._lib.lib()
+    L.blt_debug_set_tile_record.argtypes = [ctypes.c_void_p]
+    sp = torch.cuda.current_stream().cuda_stream
+    for it in range(3):
+        L.blt_debug_set_tile_record(dbg.data_ptr() if it == 2 else None)
+        s.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
+    L.blt_debug_set_tile_record(None)
+    rec = dbg.cpu().numpy().astype(np.int64)
+    how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
+    st = rec[4 * ntiles:].reshape(ntiles, 4)
+    p1, p2, p3 = st[:, 1] - st[:, 0], st[:, 2] - st[:, 1], st[:, 3] - st[:, 2]
+    tot = st[:, 3] - st[:, 0]
+    for name, v in (("phase1", p1), ("phase2", p2), ("phase3", p3), ("tile", tot)):
+        print(f"{name:7s} mean {v.mean():9.0f}  median {np.median(v):9.0f}  p90 {np.percentile(v, 90):9.0f} cycles")
+    f = how & 0xFF
+    win = how >> 8
+    valid = how != 0xFFFF
+    print("look-back: first-inclusive lane mean %.1f, windows mean %.2f max %d" %
+          (f[valid].mean(), (win[valid] / 64 + 1).mean(), (win[valid] // 64 + 1).max()))
+    span = st[:, 3].max() - st[:, 0].min()
+    print(f"kernel span {span} cycles; tiles per CU ~{ntiles / 256:.0f}")
+
+
+if __name__ == "__main__":
+    main()
