@@ -192,8 +192,9 @@ constexpr int kMaxDevices = 64;
 struct DevTables {
     std::once_flag once;
     int status = 0;
-    uint16_t* dense = nullptr;      // native u16 values
-    uint16_t* dense_be = nullptr;   // byte-swapped values (big-endian byte pass)
+    uint16_t* dense = nullptr;      // native u16 values, sentinel where absent (general kernel)
+    uint16_t* self_ne = nullptr;    // self-token table, native byte order (byte-pass kernel)
+    uint16_t* self_be = nullptr;    // self-token table, output (big-endian) byte order
     uint64_t* hslots = nullptr;
 };
 
@@ -201,9 +202,11 @@ struct blt_bpe {
     size_t n_entries = 0;
     bool single_pass = true;
     uint32_t sentinel = 0;                 // > 0xFFFF: every byte pair is a merge
-    uint32_t sentinel_be = 0;              // the sentinel in output (big-endian) byte order
     std::vector<uint16_t> dense;           // 65536, swizzled (blt::dense_index)
-    std::vector<uint16_t> dense_be;        // the same with byte-swapped values
+    // Self-token tables of the byte-pass kernel: entry (a, b) = merged token, or a itself when
+    // (a, b) is no merge.  Usable when no byte-pair key (a, b) maps to a (self_ok).
+    bool self_ok = true;
+    std::vector<uint16_t> self_ne, self_be;
     std::vector<uint64_t> hslots;          // general map, empty when single_pass
     uint64_t hmask = 0;
     DevTables dev[kMaxDevices];
@@ -250,9 +253,18 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
         if (a < 256 && b < 256) h->dense[blt::dense_index(a, b)] = kv.second;
     }
     auto bswap = [](uint32_t v) { return (uint16_t)(((v & 0xFF) << 8) | ((v >> 8) & 0xFF)); };
-    h->sentinel_be = h->sentinel > 0xFFFF ? h->sentinel : bswap(h->sentinel);
-    h->dense_be.resize(65536);
-    for (int i = 0; i < 65536; ++i) h->dense_be[i] = bswap(h->dense[i]);
+    h->self_ne.resize(65536);
+    for (uint32_t a = 0; a < 256; ++a)
+        for (uint32_t b = 0; b < 256; ++b) h->self_ne[blt::dense_index(a, b)] = (uint16_t)a;
+    for (const auto& kv : map) {
+        const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
+        if (a < 256 && b < 256) {
+            h->self_ne[blt::dense_index(a, b)] = kv.second;
+            if (kv.second == a) h->self_ok = false;
+        }
+    }
+    h->self_be.resize(65536);
+    for (int i = 0; i < 65536; ++i) h->self_be[i] = bswap(h->self_ne[i]);
     if (!h->single_pass) {
         uint64_t cap = 16;
         while (cap < 2 * (uint64_t)map.size() + 2) cap <<= 1;
@@ -287,8 +299,11 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
                   hipMalloc(&t.dense, 65536 * sizeof(uint16_t)) == hipSuccess &&
                   hipMemcpyAsync(t.dense, h->dense.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice, us) ==
                       hipSuccess &&
-                  hipMalloc(&t.dense_be, 65536 * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.dense_be, h->dense_be.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                  hipMalloc(&t.self_ne, 65536 * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.self_ne, h->self_ne.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                                 us) == hipSuccess &&
+                  hipMalloc(&t.self_be, 65536 * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.self_be, h->self_be.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
                                  us) == hipSuccess;
         if (ok && !h->hslots.empty()) {
             const size_t bytes = h->hslots.size() * sizeof(uint64_t);
@@ -360,7 +375,7 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
              uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false) {
-    const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes;   // the byte-pass fast kernel
+    const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->self_ok;   // byte-pass fast kernel
     const uint64_t tile = columnar ? blt::kTilePosBytes : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
@@ -378,8 +393,8 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     p.total = reinterpret_cast<uint64_t*>(ws + L.total);
     p.ntiles = (uint32_t)ntiles;
-    p.sentinel = (columnar && be) ? h->sentinel_be : h->sentinel;
-    p.dense = (columnar && be) ? t->dense_be : t->dense;
+    p.sentinel = h->sentinel;
+    p.dense = columnar ? (be ? t->self_be : t->self_ne) : t->dense;
     p.hslots = t->hslots;
     p.hmask = h->hmask;
     p.debug = g_debug_tiles;
@@ -656,7 +671,8 @@ void blt_bpe_destroy(blt_bpe* h) {
     if (!h) return;
     for (int d = 0; d < kMaxDevices; ++d) {
         if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);
-        if (h->dev[d].dense_be) (void)hipFree(h->dev[d].dense_be);
+        if (h->dev[d].self_ne) (void)hipFree(h->dev[d].self_ne);
+        if (h->dev[d].self_be) (void)hipFree(h->dev[d].self_be);
         if (h->dev[d].hslots) (void)hipFree(h->dev[d].hslots);
     }
     delete h;

@@ -26,12 +26,14 @@ struct PassParams {
     uint64_t* total;           // number of output tokens
     uint32_t ntiles;
     uint32_t sentinel;         // dense table: "absent" value; > 0xFFFF = every byte pair present
-    const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout); for a
-                               // big-endian byte pass: values (and sentinel) byte-swapped
+    const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout).  General
+                               // kernel: native values, sentinel where absent.  Byte-pass kernel:
+                               // self-token table (absent (a, b) -> a) in the output byte order
     const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
     uint64_t hmask;
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
-                               // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime stamps
+                               // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
+                               // the iteration start, after the first and second barrier; spins
 };
 
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);

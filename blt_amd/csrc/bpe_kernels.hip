@@ -143,7 +143,8 @@ struct Fn64 {  // tile-sequence function: carry-in c -> (carry-out, count)
 
 // Wave-wide look-back for tile T (all 64 lanes of one wave).  Returns carry-in and the number
 // of tokens before tile T.
-__device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t& O, uint32_t& how) {
+__device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t& O, uint32_t& how,
+                         uint32_t* spins_out = nullptr) {
     const int lane = threadIdx.x & 63;
     Fn64 acc = {0u, 1u, 0ull, 0ull};   // function of tiles (k+1 .. T-1), identity so far
     int64_t k = (int64_t)T - 1;
@@ -179,6 +180,7 @@ __device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t&
             carry = carry ? acc.co1 : acc.co0;
             C = carry; O = off;
             how = (uint32_t)f | ((uint32_t)(T - 1 - k) << 8);
+            if (spins_out) *spins_out = spins;
             return;
         }
         // no inclusive prefix in the window: fold the 64 aggregates (tiles k-63 .. k) in front of acc
@@ -490,21 +492,32 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
 // of wave w owns 16 consecutive positions (one 16-byte load), so a wave owns 1024 contiguous
 // positions and emits them as one contiguous run of tokens.
 //
-// Phase 1 (no synchronisation): per lane, 16 table lookups from LDS, then the 16-bit merge
-// mask is scanned under BOTH carry-in hypotheses at once — carry 0 in the low 16 bits, carry 1
-// in the high 16 bits of one register, with packed 16-bit adds/shifts (see merges_for).  A
-// wave resolves its lanes' carries with two ballots and one packed prefix scan.
-// Phase 2 (one barrier): the kS x kWaves wave functions give the tile function; wave 0
-// publishes it and resolves the tile's carry-in and output offset by the decoupled look-back.
-// Phase 3 (no block barriers): each wave writes its tokens to a private LDS stage — every lane
-// writes one u16 per position in order; a consumed position writes the slot that the next
-// (landing) position then overwrites, since no two consecutive positions are both consumed —
-// and copies the stage out with 16-byte stores.  As a sub-tile's input registers free up they
-// are refilled with the next tile's bytes, so its loads fly while this tile is written.
+// Self-token table: the LDS entry of a byte pair (a, b) is its merged token when (a, b) is a
+// merge and the token of a itself otherwise (in output byte order).  A lookup then yields the
+// token position i emits if it lands, and m[i] = (entry != token of a): one bit-op per two
+// positions.  This needs no key (a, b) to map to a, which the host checks (self_ok); a
+// position whose merge is cut (chunk end, buffer end) gets its raw byte patched in.
+//
+// Phase 1 (no synchronisation): per lane, 16 lookups, then the 16-bit merge mask is scanned
+// under BOTH carry-in hypotheses at once — carry 0 in the low 16 bits, carry 1 in the high 16
+// bits of one register, packed 16-bit adds/shifts (merges_for).  A wave resolves its lanes'
+// carries with two ballots and one packed DPP prefix sum.
+//
+// Emission is deferred by one tile.  Iteration i runs phase 1 of tile T_i while wave 0 has
+// the look-back loads of the previous tile T_{i-1} in flight; after phase 1 wave 0 resolves
+// T_{i-1}'s carry-in and offset (its predecessors published their functions about one tile
+// of work earlier, so the look-back rarely waits), a barrier, then the last wave resolves and
+// publishes T_i's function while every wave writes T_{i-1}'s tokens: each lane writes one u16
+// per position into its wave's LDS stage (a consumed position writes the slot the next,
+// landing, position overwrites), and the wave copies the stage out with 16-byte buffer
+// stores; as a sub-tile is written its input registers are refilled with the next tile's
+// bytes.  The look-back reads 4 windows of 64 status words per round trip and folds them with
+// ballots and a wave sum.
 // ===========================================================================================
 namespace seg {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t pk_shl1(uint32_t v) {
     const u16x2 r = __builtin_bit_cast(u16x2, v) << (u16x2){1, 1};            // v_pk_lshlrev_b16
     return __builtin_bit_cast(uint32_t, r);
@@ -512,6 +525,12 @@ __device__ __forceinline__ uint32_t pk_shl1(uint32_t v) {
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
     const u16x2 r = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);   // v_pk_add_u16
     return __builtin_bit_cast(uint32_t, r);
+}
+// Each 16-bit half -> 1 if nonzero, else 0 (the compiler would expand min into compares).
+__device__ __forceinline__ uint32_t pk_nz(uint32_t v) {
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "s"(0x00010001u));
+    return r;
 }
 
 constexpr int kThreads = 512;
@@ -521,6 +540,9 @@ constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
 constexpr int kStageWave = 2 * (int)kWavePos + 32;     // tokens + 16-byte alignment slack
+constexpr int kLbWin = 4;                              // look-back windows of 64 per round trip
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kLbSpinLimit = 1u << 18;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
 static_assert(kGroups <= 64, "one lane per group in the tile resolve");
@@ -531,14 +553,17 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
 }
 
-// Buffer resource over in[base, n) (records clamped): out-of-range loads return 0.  Built from
-// wave-uniform values only, so the loads need no waterfall loop (cdna guide T20).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* in, uint64_t base, uint64_t n) {
-    const uint64_t left = base < n ? n - base : 0;
+// Buffer resource over base[0, left) (records clamped to 2^31 - 1): out-of-range loads return
+// 0 and out-of-range stores are dropped.  Built from wave-uniform values only, so the accesses
+// need no waterfall loop (cdna guide T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* base, uint64_t left) {
     const uint32_t records = uni((uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left));
-    const uint64_t addr = uni64((uint64_t)(uintptr_t)(in + (base < n ? base : 0)));
+    const uint64_t addr = uni64((uint64_t)(uintptr_t)base);
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uintptr_t)addr), (short)0, (int)records,
                                              0x00020000);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* in, uint64_t base, uint64_t n) {
+    return rsrc_at(in + (base < n ? base : 0), base < n ? n - base : 0);
 }
 
 // A lane's 16 bytes at byte `off` of the resource; the byte after the wave's range for lane 63.
@@ -561,15 +586,305 @@ __device__ __forceinline__ void load_sub(__amdgpu_buffer_rsrc_t r, bool full, in
     nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)kWavePos, 0, 0);
 }
 
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {   // lanes without a source read 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+// Inclusive wave-wide prefix sum: row_shr 1/2/4/8 within rows, then row_bcast 15 and 31.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+    v += dpp0<0x111>(v);
+    v += dpp0<0x112>(v);
+    v += dpp0<0x114>(v);
+    v += dpp0<0x118>(v);
+    v += dpp0<0x142, 0xA>(v);
+    v += dpp0<0x143, 0xC>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int i) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+}
+
+// ---- phase 1 of one sub-tile: lookups, lane function, wave function --------------------------
+template <bool kBE>
+__device__ __forceinline__ void phase1_sub(const uint16_t* s_tab, const uint32_t (&x)[4], uint32_t nxt,
+                                           uint64_t wb, uint64_t n, uint64_t bnext, int lane, uint32_t (&vals)[8],
+                                           uint32_t& mv, uint32_t& lw, uint32_t& ex, uint32_t* wfn) {
+    const uint32_t lo16 = 16u * (uint32_t)lane;
+    // positions left in the buffer from this wave's first one (clamped: uniform 32-bit)
+    const uint32_t rem = wb >= n ? 0u : (n - wb > 2u * kWavePos ? 2u * kWavePos : (uint32_t)(n - wb));
+    // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63 keeps the
+    // "old" operand, the byte after the wave's range
+    const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false) & 0xFFu;
+    uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
+        const uint32_t lo = x[h >> 1], hi = (h >> 1) < 3 ? x[(h >> 1) + 1] : nb;
+        const uint32_t t0 = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
+        const uint32_t t = t0 ^ ((t0 >> 7) & 0x00FE00FEu);            // bank swizzle of b
+        const uint32_t v = (uint32_t)s_tab[t & 0xFFFFu] | ((uint32_t)s_tab[t >> 16] << 16);
+        vals[h] = v;
+        // token of a itself, in output byte order: BE (a << 8), native a
+        const uint32_t self = kBE ? (t0 & 0xFF00FF00u) : ((t0 >> 8) & 0x00FF00FFu);
+        m32 |= pk_nz(v ^ self) << (2 * h);
+    }
+    uint32_t m = (m32 & 0xFFFFu) | (m32 >> 15);
+    // valid positions, right neighbours inside the buffer, chunk ends
+    const int32_t r = (int32_t)rem - (int32_t)lo16;                   // positions left from mine
+    const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
+    m &= (vmask >> 1) | (r > 16 ? 0x8000u : 0u);
+    uint32_t forced = (r >= 1 && r <= 16) ? (1u << (r - 1)) : 0u;     // the buffer's last position
+    if (bnext < n && bnext - 1 - wb < kWavePos) {                     // chunk end b - 1 here
+        const uint32_t e = (uint32_t)(bnext - 1 - wb) - lo16;
+        if (e < 16u) { m &= ~(1u << e); forced |= 1u << e; }
+    }
+    if (__ballot(forced != 0)) {   // rare: a cut merge emits its raw byte
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const uint32_t xw = x[h >> 1];
+            const uint32_t raw = __builtin_amdgcn_perm(xw, xw, kBE ? ((h & 1) ? 0x030C020Cu : 0x010C000Cu)
+                                                                   : ((h & 1) ? 0x0C030C02u : 0x0C010C00u));
+            const uint32_t fm = (((forced >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) |
+                                (((forced >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
+            vals[h] = (vals[h] & ~fm) | (raw & fm);
+        }
+    }
+    mv = m | (vmask << 16);
+    // lane function, both carry-in hypotheses: low half c = 0 (position 0 consumed), high
+    // half c = 1 (merges_for, packed 16-bit)
+    const uint32_t mc = (m & ~1u) | (m << 16);
+    const uint32_t st = mc & ~pk_shl1(mc);
+    const uint32_t rodd = mc & ~pk_add(mc, st & 0xAAAAAAAAu);
+    const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
+    const uint32_t L = ~(pk_shl1(M) | 1u) & (vmask | (vmask << 16));
+    const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
+    const uint32_t cout = ((M >> 31) & 1u) ^ 1u;                     // carry-out if not identity
+    const uint32_t ident = m == 0xFFFFu;
+    // wave resolve
+    const uint64_t nonid = __ballot(!ident);
+    const uint64_t cmask = __ballot(cout);
+    const uint64_t below = nonid & ((1ull << lane) - 1ull);
+    const uint32_t hb = below != 0;
+    const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
+    const uint32_t c0 = hb ? bc : 0u, c1 = hb ? bc : 1u;
+    const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
+    const uint32_t incl = wave_scan(packed);
+    ex = incl - packed;
+    lw = hb | (bc << 1);
+    if (lane == 63) {
+        wfn[0] = nonid == 0;
+        wfn[1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+        wfn[2] = incl & 0xFFFFu;
+        wfn[3] = incl >> 16;
+    }
+}
+
+// ---- tile resolve (one wave): group carries and offsets, tile function, publish -------------
+__device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane, const uint32_t (*wfn)[4],
+                                             uint32_t (*gin)[4], uint32_t* tfn) {
+    uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
+    if (lane < kGroups) { gi = wfn[lane][0]; gco = wfn[lane][1]; g0 = wfn[lane][2]; g1 = wfn[lane][3]; }
+    const uint64_t nonid = __ballot(!gi);
+    const uint64_t cmask = __ballot(gco);
+    const uint64_t below = nonid & ((1ull << lane) - 1ull);
+    const uint32_t hb = below != 0;
+    const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
+    const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
+    // a tile has at most 32768 tokens per hypothesis: both fit one packed scan
+    const uint32_t my = (cin0 ? g1 : g0) | ((cin1 ? g1 : g0) << 16);
+    const uint32_t inc = wave_scan(my);
+    const uint32_t exc = inc - my;
+    if (lane < kGroups) {
+        gin[lane][0] = cin0;
+        gin[lane][1] = cin1;
+        gin[lane][2] = exc & 0xFFFFu;
+        gin[lane][3] = exc >> 16;
+    }
+    const uint32_t tot = lane_u32(inc, 63);
+    const uint32_t tot0 = tot & 0xFFFFu, tot1 = tot >> 16;
+    const uint32_t tident = nonid == 0;
+    const uint32_t tcout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+    const uint32_t co0 = tident ? 0u : tcout, co1 = tident ? 1u : tcout;
+    if (lane == 0) {
+        tfn[0] = co0; tfn[1] = co1; tfn[2] = tot0; tfn[3] = tot1;
+        // tile 0 starts with carry 1 at offset 0: its inclusive prefix is known at once
+        st_publish(p.status + T, T == 0 ? st_incl(co1, tot1) : st_agg(co0, co1, tot0, tot1));
+    }
+}
+
+// ---- look-back (wave 0) ------------------------------------------------------------------
+// Lane l of window q reads the status of tile k - l - 64 q; tiles before 0 read as an
+// inclusive prefix with carry 1 at offset 0.
+__device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lane, uint64_t (&s)[kLbWin]) {
+#pragma unroll
+    for (int q = 0; q < kLbWin; ++q) {
+        const int64_t idx = k - lane - 64 * q;
+        s[q] = idx >= 0 ? st_read(p.status + idx) : st_incl(1u, 0ull);
+    }
+}
+
+// Function of the aggregates in lanes [0, lim) of one window (lane 0 newest) applied to
+// carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.
+__device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot) {
+    const bool in = lane < lim;
+    const uint32_t co0 = (uint32_t)(s >> 60) & 1u, co1 = (uint32_t)(s >> 61) & 1u;
+    const bool ident = co0 == 0u && co1 == 1u;
+    const uint64_t nonid = __ballot(in && !ident);
+    const uint64_t comask = __ballot(in && co0);   // a non-identity function is constant
+    const uint64_t older = nonid & ~((~0ull) >> (63 - lane));
+    const uint32_t cin = older ? (uint32_t)((comask >> __builtin_ctzll(older)) & 1ull) : c;
+    const uint32_t cnt = in ? (uint32_t)(cin ? (s >> 30) & 0x3FFFFFFFull : s & 0x3FFFFFFFull) : 0u;
+    tot += lane_u32(wave_scan(cnt), 63);
+    return nonid ? (uint32_t)((comask >> __builtin_ctzll(nonid)) & 1ull) : c;
+}
+
+struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never indexed (no alloca)
+    uint32_t co0, co1;
+    uint64_t t0, t1;
+};
+
+__device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (&s)[kLbWin], uint32_t& C,
+                          uint64_t& O, uint32_t& how, uint32_t& spins) {
+    TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
+    int64_t k = (int64_t)Tp - 1;
+    uint32_t rounds = 0;
+    for (;;) {
+        int qs = -1, f = 64;
+        bool ready = true;
+#pragma unroll
+        for (int q = 0; q < kLbWin; ++q) {
+            const uint32_t flag = (uint32_t)(s[q] >> 62);
+            const uint64_t inc = __ballot(flag == 2u), rdy = __ballot(flag != 0u);
+            if (qs < 0) {
+                if (inc) {
+                    f = __builtin_ctzll(inc);
+                    const uint64_t need = (~0ull) >> (63 - f);
+                    if ((rdy & need) != need) ready = false;
+                    qs = q;
+                } else if (rdy != ~0ull) {
+                    ready = false;
+                }
+            }
+        }
+        if (!ready) {
+            if (++spins > kLbSpinLimit) {
+                if (lane == 0) atomicOr(p.ctl + 1, 1u);
+                C = 1u; O = 0ull;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            lb_issue(p, k, lane, s);
+            continue;
+        }
+        if (qs < 0) {   // no inclusive prefix in 256 tiles: fold them into acc, read further back
+            TileFn w;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t c = (uint32_t)h;
+                uint64_t t = 0;
+#pragma unroll
+                for (int q = kLbWin - 1; q >= 0; --q) c = win_apply(s[q], 64, lane, c, t);
+                t += c ? acc.t1 : acc.t0;
+                if (h == 0) { w.co0 = c ? acc.co1 : acc.co0; w.t0 = t; }
+                else { w.co1 = c ? acc.co1 : acc.co0; w.t1 = t; }
+            }
+            acc = w;
+            k -= 64 * kLbWin;
+            ++rounds;
+            lb_issue(p, k, lane, s);
+            continue;
+        }
+        uint32_t c = 0;
+        uint64_t off = 0;
+#pragma unroll
+        for (int q = kLbWin - 1; q >= 0; --q) {
+            if (q > qs) continue;
+            if (q == qs) {
+                const uint64_t sf = ((uint64_t)lane_u32((uint32_t)(s[q] >> 32), f) << 32) | lane_u32((uint32_t)s[q], f);
+                c = (uint32_t)(sf >> 61) & 1u;
+                off = sf & ((1ull << 61) - 1ull);
+                c = win_apply(s[q], f, lane, c, off);
+            } else {
+                c = win_apply(s[q], 64, lane, c, off);
+            }
+        }
+        O = off + (c ? acc.t1 : acc.t0);
+        C = c ? acc.co1 : acc.co0;
+        how = (uint32_t)f | ((uint32_t)qs << 6) | (rounds << 8);
+        return;
+    }
+}
+
+// ---- emission of one sub-tile of the pending tile -------------------------------------------
+__device__ __forceinline__ void emit_sub(const PassParams& p, uint32_t Tp, uint32_t j, uint32_t wave, int lane,
+                                         const uint32_t (&vals)[8], uint32_t mv, uint32_t lw, uint32_t ex,
+                                         const uint32_t* gin, uint32_t C, uint64_t O, uint64_t wb, uint64_t& cnext,
+                                         uint8_t* st, uint8_t* out) {
+    const uint64_t n = p.n, cs = p.cs;
+    const uint32_t cg = uni(gin[C]);
+    const uint64_t og = O + uni(gin[2 + C]);                 // wave's first token
+    const uint32_t m = mv & 0xFFFFu, vmask = mv >> 16;
+    const uint32_t c = (lw & 1u) ? (lw >> 1) : cg;
+    const uint32_t lane_off = cg ? (ex >> 16) : (ex & 0xFFFFu);
+    const uint32_t mc = c ? m : (m & ~1u);
+    const uint32_t sst = mc & ~(mc << 1);
+    const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
+    const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+    const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
+    const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
+    const uint64_t gb = 2ull * og;
+    const uint64_t ab = gb & ~15ull;
+    const uint32_t rg = (uint32_t)(gb - ab);
+    uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
+    uint32_t a = rg + 2u * lane_off;                     // stage byte of this lane's next token
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const uint32_t k = 2u * (uint32_t)h;
+        const uint32_t tok = vals[h];
+        st16[a >> 1] = (uint16_t)tok;
+        a += 2u * ((L >> k) & 1u);
+        if (h < 7 || ((L >> 15) & 1u)) st16[a >> 1] = (uint16_t)(tok >> 16);
+        a += 2u * ((L >> (k + 1)) & 1u);
+    }
+    // token index of a chunk start in this lane's segment
+    while (cnext < wb) cnext += cs;
+    if (p.chunk_off && cnext < n && cnext - wb < kWavePos) {
+        const uint32_t e = (uint32_t)(cnext - wb) - 16u * (uint32_t)lane;
+        if (e < 16u) p.chunk_off[cnext / cs] = og + lane_off + __popc(L & ((1u << e) - 1u));
+    }
+    // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each, lanes
+    // 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order LDS queue).
+    const uint32_t re = rg + 2u * wcnt;
+    if (ab + re > p.out_cap) {
+        if (lane == 0) record_error(p, 2u, Tp, j, O, ab + re, C);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + ab, p.out_cap - ab);
+    const uint32_t hend = ((rg + 15u) & ~15u) < re ? ((rg + 15u) & ~15u) : re;
+    const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
+    const uint32_t nfull = (tbeg - hend) >> 4;
+    for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
+        const uint32_t o = hend + 16u * i;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(st + o);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)o, 0, 0);
+    }
+    if (lane < 16) {
+        const uint32_t o = lane < 8 ? rg + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+        const uint32_t lim = lane < 8 ? hend : re;
+        if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)o, 0, 0);
+    }
+}
+
 template <bool kBE>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
-    __shared__ uint32_t s_wfn[kGroups][4];    // ident, cout, cnt|c=0, cnt|c=1
-    __shared__ uint32_t s_gin[kGroups][4];    // carry-in |H=0, |H=1, offset |H=0, |H=1
+    __shared__ uint32_t s_wfn[kGroups][4];       // wave functions of the tile in phase 1
+    __shared__ uint32_t s_gin[2][kGroups][4];    // per slot: group carry-in |H=0,1, offset |H=0,1
+    __shared__ uint32_t s_tfn[2][4];             // per slot: tile co0, co1, tot0, tot1
     __shared__ uint32_t s_C;
     __shared__ uint64_t s_O;
-    __shared__ uint32_t s_ticket[2];
+    __shared__ uint32_t s_ticket;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -577,12 +892,11 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t n = p.n, cs = p.cs;
-    const uint32_t S = p.sentinel;              // table's "absent" (0x10000: every pair merges)
     const uint32_t ntiles = p.ntiles;
 
     if (tid == 0) {
-        s_ticket[0] = atomicAdd(p.ctl, 1u);
-        s_ticket[1] = atomicAdd(p.ctl, 1u);
+        s_wfn[0][0] = atomicAdd(p.ctl, 1u);
+        s_wfn[0][1] = atomicAdd(p.ctl, 1u);
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
@@ -590,10 +904,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
     }
     __syncthreads();
-    uint32_t T = uni(s_ticket[0]);
-    uint32_t Tn = uni(s_ticket[1]);
+    uint32_t T = uni(s_wfn[0][0]);    // tile in phase 1
+    uint32_t Tn = uni(s_wfn[0][1]);   // tile whose bytes are loaded during this iteration's emission
+    uint32_t Tp = kNone;              // tile waiting for emission
+    __syncthreads();
 
-    uint32_t x[kS][4];      // input bytes of each sub-tile
+    uint32_t x[kS][4];      // input bytes of each sub-tile of T
     uint32_t nxt[kS];       // byte after this wave's range (lane 63's right neighbour)
     if (T < ntiles) {
 #pragma unroll
@@ -602,223 +918,108 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             load_sub(rsrc(in, wb, n), wb + kWavePos <= n, lane, x[j], nxt[j]);
         }
     }
+    uint32_t vp[kS][8], mvp[kS], lwp[kS], exq[kS];   // phase-1 state of Tp
+    uint32_t slot = 0;                               // s_gin / s_tfn slot of T (Tp has slot ^ 1)
 
-    while (T < ntiles) {
-        const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
+    while (T < ntiles || Tp < ntiles) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         const uint64_t ts0 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
-        uint32_t vals[kS][8];   // looked-up values (output byte order), two per register
-        uint32_t mv[kS];        // merge mask | valid mask << 16
-        uint32_t lw[kS];        // bit 0: a non-identity lane below; bit 1: its carry-out
-        uint32_t ex[kS];        // exclusive prefix count, carry-in 0 | carry-in 1 << 16
+        // look-back loads for Tp fly during phase 1 (wave 0); ticket for the tile after Tn
+        uint64_t lbs[kLbWin];
+        const bool lb = wave == 0 && Tp < ntiles && Tp > 0;
+        if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+        uint32_t tk = kNone;
+        if (tid == 64 && Tn < ntiles) tk = atomicAdd(p.ctl, 1u);
+        asm volatile("" ::: "memory");
 
-        // first chunk start > this wave's first position; advanced monotonically below
-        uint64_t bnext = uni64(((tile0 + (uint64_t)wave * kWavePos) / cs + 1) * cs);
-
-        // ---- phase 1: lookups, lane functions, wave functions ---------------------------------
+        // ---- phase 1 of T -------------------------------------------------------------------
+        uint32_t vc[kS][8], mvc[kS], lwc[kS], exc[kS];
+        if (T < ntiles) {
+            const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
+            // first chunk start > this wave's first position; advanced monotonically
+            uint64_t bnext = uni64(((tile0 + (uint64_t)wave * kWavePos) / cs + 1) * cs);
 #pragma unroll
-        for (int j = 0; j < kS; ++j) {
-            const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-            const uint32_t lo16 = 16u * (uint32_t)lane;
-            while (bnext <= wb) bnext += cs;
-            // positions left in the buffer from this wave's first one (clamped: uniform 32-bit)
-            const uint32_t rem = wb >= n ? 0u : (n - wb > 2u * kWavePos ? 2u * kWavePos : (uint32_t)(n - wb));
-            // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63
-            // keeps the "old" operand, the byte after the wave's range
-            const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt[j], (int)x[j][0], 0x130, 0xF, 0xF,
-                                                                      false) & 0xFFu;
-            uint32_t m = 0;
-#pragma unroll
-            for (int h = 0; h < 8; ++h) {
-                // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
-                const uint32_t lo = x[j][h >> 1], hi = (h >> 1) < 3 ? x[j][(h >> 1) + 1] : nb;
-                const uint32_t t0 = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
-                const uint32_t t = t0 ^ ((t0 >> 7) & 0x00FE00FEu);            // bank swizzle of b
-                const uint32_t va = s_tab[t & 0xFFFFu];
-                const uint32_t vb = s_tab[t >> 16];
-                vals[j][h] = va | (vb << 16);
-                m |= ((uint32_t)(va != S) << (2 * h)) | ((uint32_t)(vb != S) << (2 * h + 1));
-            }
-            // valid positions, right neighbours inside the buffer, chunk ends
-            const int32_t r = (int32_t)rem - (int32_t)lo16;                   // positions left from mine
-            const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
-            m &= (vmask >> 1) | (r > 16 ? 0x8000u : 0u);
-            if (bnext < n && bnext - 1 - wb < kWavePos) {                     // chunk end b - 1 here
-                const uint32_t e = (uint32_t)(bnext - 1 - wb) - lo16;
-                if (e < 16u) m &= ~(1u << e);
-            }
-            mv[j] = m | (vmask << 16);
-            // lane function, both carry-in hypotheses: low half c = 0 (position 0 consumed),
-            // high half c = 1 (merges_for, packed 16-bit)
-            const uint32_t mc = (m & ~1u) | (m << 16);
-            const uint32_t st = mc & ~pk_shl1(mc);
-            const uint32_t rodd = mc & ~pk_add(mc, st & 0xAAAAAAAAu);
-            const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
-            const uint32_t L = ~(pk_shl1(M) | 1u) & (vmask | (vmask << 16));
-            const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
-            const uint32_t cout = ((M >> 31) & 1u) ^ 1u;                     // = carry-0 one if not identity
-            const uint32_t ident = m == 0xFFFFu;
-            // wave resolve
-            const uint64_t nonid = __ballot(!ident);
-            const uint64_t cmask = __ballot(cout);
-            const uint64_t below = nonid & ((1ull << lane) - 1ull);
-            const uint32_t hb = below != 0;
-            const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
-            const uint32_t c0 = hb ? bc : 0u, c1 = hb ? bc : 1u;
-            const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
-            const uint32_t incl = wave_incl_scan(packed, lane);
-            ex[j] = incl - packed;
-            lw[j] = hb | (bc << 1);
-            if (lane == 63) {
-                const uint32_t g = (uint32_t)j * kWaves + wave;
-                s_wfn[g][0] = nonid == 0;
-                s_wfn[g][1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
-                s_wfn[g][2] = incl & 0xFFFFu;
-                s_wfn[g][3] = incl >> 16;
+            for (int j = 0; j < kS; ++j) {
+                const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+                while (bnext <= wb) bnext += cs;
+                phase1_sub<kBE>(s_tab, x[j], nxt[j], wb, n, bnext, lane, vc[j], mvc[j], lwc[j], exc[j],
+                                s_wfn[(uint32_t)j * kWaves + wave]);
             }
         }
+
+        // ---- carry-in and offset of Tp (wave 0) --------------------------------------------
+        uint32_t spins = 0;
+        if (wave == 0 && Tp < ntiles) {
+            uint32_t C = 1u, how = 0xFFFFu;
+            uint64_t O = 0ull;
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+            if (lane == 0) {
+                const uint32_t* tf = s_tfn[slot ^ 1u];
+                const uint64_t tot = C ? tf[3] : tf[2];
+                const uint64_t end = O + tot;
+                if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
+                    record_error(p, 4u, Tp, 0xFFu, O, end, C);
+                    O = 0; C = 1;
+                }
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf[1] : tf[0], O + (C ? tf[3] : tf[2])));
+                s_C = C;
+                s_O = O;
+                if (Tp == ntiles - 1) {
+                    *p.total = O + (C ? tf[3] : tf[2]);
+                    if (p.chunk_off) p.chunk_off[p.nchunks] = O + (C ? tf[3] : tf[2]);
+                }
+                if (p.debug) {
+                    uint64_t* d = p.debug + 4ull * Tp;
+                    d[0] = O;
+                    d[1] = ((uint64_t)C << 32) | how;
+                    d[2] = ((uint64_t)tf[3] << 32) | tf[2];
+                    d[3] = ((uint64_t)tf[1] << 32) | tf[0];
+                }
+            }
+        }
+        if (tid == 64) s_ticket = tk;
         __syncthreads();
         const uint64_t ts1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
 
-        // ---- phase 2: tile function, publish, look-back (wave 0) ------------------------------
-        if (wave == 0) {
-            uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
-            if (lane < kGroups) { gi = s_wfn[lane][0]; gco = s_wfn[lane][1]; g0 = s_wfn[lane][2]; g1 = s_wfn[lane][3]; }
-            const uint64_t nonid = __ballot(!gi);
-            const uint64_t cmask = __ballot(gco);
-            const uint64_t below = nonid & ((1ull << lane) - 1ull);
-            const uint32_t hb = below != 0;
-            const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
-            const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
-            const uint32_t my0 = cin0 ? g1 : g0, my1 = cin1 ? g1 : g0;
-            const uint32_t inc0 = wave_incl_scan(my0, lane), inc1 = wave_incl_scan(my1, lane);
-            if (lane < kGroups) {
-                s_gin[lane][0] = cin0;
-                s_gin[lane][1] = cin1;
-                s_gin[lane][2] = inc0 - my0;
-                s_gin[lane][3] = inc1 - my1;
-            }
-            const uint32_t tot0 = __shfl(inc0, 63, 64), tot1 = __shfl(inc1, 63, 64);
-            const uint32_t tident = nonid == 0;
-            const uint32_t tcout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
-            const uint32_t co0 = tident ? 0u : tcout, co1 = tident ? 1u : tcout;
-            uint32_t C;
-            uint64_t O;
-            uint32_t how = 0xFFFFu;
-            if (T == 0) {
-                C = 1u; O = 0ull;
-            } else {
-                if (lane == 0) st_publish(p.status + T, st_agg(co0, co1, tot0, tot1));
-                lookback(p, T, C, O, how);
-            }
-            if (lane == 0) {
-                const uint64_t end = O + (C ? tot1 : tot0);
-                if (O > tile0 || end > n) {
-                    record_error(p, 4u, T, 0xFFu, O, end, C);
-                    O = 0; C = 1;
-                }
-                st_publish(p.status + T, st_incl(C ? co1 : co0, end));
-                s_C = C; s_O = O;
-                if (T == ntiles - 1) {
-                    *p.total = end;
-                    if (p.chunk_off) p.chunk_off[p.nchunks] = end;
-                }
-                if (p.debug) {
-                    uint64_t* d = p.debug + 4ull * T;
-                    d[0] = O;
-                    d[1] = ((uint64_t)C << 32) | how;
-                    d[2] = ((uint64_t)tot1 << 32) | tot0;
-                    d[3] = ((uint64_t)co1 << 32) | co0;
-                }
-            }
-        }
-        if (tid == 64) s_ticket[0] = atomicAdd(p.ctl, 1u);   // the tile after Tn
-        __syncthreads();
-        const uint64_t ts2 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
+        // ---- resolve and publish T (last wave) ----------------------------------------------
+        if (wave == kWaves - 1 && T < ntiles) resolve_tile(p, T, lane, s_wfn, s_gin[slot], s_tfn[slot]);
 
-        // ---- phase 3: emit each sub-tile's tokens; refill registers with tile Tn -------------
+        // ---- emit Tp; refill registers with Tn ---------------------------------------------
         {
             const uint32_t C = uni(s_C);
             const uint64_t O = uni64(s_O);
-            // first chunk start >= this wave's first position; advanced monotonically below
-            uint64_t cnext = uni64(((tile0 + (uint64_t)wave * kWavePos + cs - 1) / cs) * cs);
-            uint8_t* st = s_stage[wave];
-            uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
+            const uint64_t tile0p = (uint64_t)(Tp < ntiles ? Tp : 0) * kTilePosBytes;
+            uint64_t cnext = 0;
+            if (Tp < ntiles) cnext = uni64(((tile0p + (uint64_t)wave * kWavePos + cs - 1) / cs) * cs);
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
                 const uint32_t g = (uint32_t)j * kWaves + wave;
-                const uint32_t cg = uni(s_gin[g][C]);
-                const uint64_t og = O + uni(s_gin[g][2 + C]);            // wave's first token
-                const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-                const uint32_t m = mv[j] & 0xFFFFu, vmask = mv[j] >> 16;
-                const uint32_t c = (lw[j] & 1u) ? (lw[j] >> 1) : cg;
-                const uint32_t lane_off = cg ? (ex[j] >> 16) : (ex[j] & 0xFFFFu);
-                const uint32_t mc = c ? m : (m & ~1u);
-                const uint32_t sst = mc & ~(mc << 1);
-                const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
-                const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
-                const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
-                const uint32_t my_cnt = __popc(L);
-                const uint32_t wcnt = uni((uint32_t)__shfl(lane_off + my_cnt, 63, 64));
-                const uint64_t gb = 2ull * og;
-                const uint64_t ab = gb & ~15ull;
-                // byte address in the stage of this lane's next token
-                uint32_t a = (uint32_t)(gb - ab) + 2u * lane_off;
-#pragma unroll
-                for (int h = 0; h < 8; ++h) {
-                    const uint32_t k = 2u * (uint32_t)h;
-                    const uint32_t xw = x[j][h >> 1];
-                    // raw bytes k, k+1 as tokens: BE [0, x] or native [x, 0] per 16-bit half
-                    const uint32_t xp = __builtin_amdgcn_perm(xw, xw, kBE ? ((h & 1) ? 0x030C020Cu : 0x010C000Cu)
-                                                                          : ((h & 1) ? 0x0C030C02u : 0x0C010C00u));
-                    const uint32_t mlo = (uint32_t)__builtin_amdgcn_sbfe((int)M, (int)k, 1);
-                    const uint32_t mhi = (uint32_t)__builtin_amdgcn_sbfe((int)M, (int)k + 1, 1);
-                    const uint32_t msk = __builtin_amdgcn_perm(mhi, mlo, 0x05040100u);
-                    const uint32_t tok = (vals[j][h] & msk) | (xp & ~msk);
-                    st16[a >> 1] = (uint16_t)tok;
-                    a += 2u * ((L >> k) & 1u);
-                    if (h < 7 || ((L >> 15) & 1u)) st16[a >> 1] = (uint16_t)(tok >> 16);
-                    a += 2u * ((L >> (k + 1)) & 1u);
+                if (Tp < ntiles) {
+                    const uint64_t wb = tile0p + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
+                    emit_sub(p, Tp, (uint32_t)j, wave, lane, vp[j], mvp[j], lwp[j], exq[j], s_gin[slot ^ 1u][g], C, O,
+                             wb, cnext, s_stage[wave], out);
                 }
-                // token index of a chunk start in this lane's segment
-                while (cnext < wb) cnext += cs;
-                if (p.chunk_off && cnext < n && cnext - wb < kWavePos) {
-                    const uint32_t e = (uint32_t)(cnext - wb) - 16u * (uint32_t)lane;
-                    if (e < 16u) p.chunk_off[cnext / cs] = og + lane_off + __popc(L & ((1u << e) - 1u));
-                }
-                // refill this sub-tile's registers with tile Tn (loads fly during the copy-out)
                 if (Tn < ntiles) {
                     const uint64_t nb2 = (uint64_t)Tn * kTilePosBytes + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
                     load_sub(rsrc(in, nb2, n), nb2 + kWavePos <= n, lane, x[j], nxt[j]);
                 }
-                // stage -> global (this wave wrote the stage: wait for its LDS writes)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const uint64_t ge = gb + 2ull * wcnt;
-                if (ge > p.out_cap) {
-                    if (lane == 0) record_error(p, 2u, T, g, O, ge, C);
-                } else {
-                    const uint32_t nblk = (uint32_t)((ge - ab + 15) >> 4);
-                    for (uint32_t i = (uint32_t)lane; i < nblk; i += 64) {
-                        const uint64_t B = ab + 16ull * i;
-                        if (B >= gb && B + 16 <= ge) {
-                            *reinterpret_cast<uint4*>(out + B) = *reinterpret_cast<const uint4*>(st + 16 * i);
-                        } else {
-                            for (int u = 0; u < 8; ++u) {
-                                const uint64_t bb = B + 2ull * u;
-                                if (bb >= gb && bb < ge) *reinterpret_cast<uint16_t*>(out + bb) = st16[8 * i + u];
-                            }
-                        }
-                    }
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         }
-        if (p.debug && tid == 0) {
-            uint64_t* d = p.debug + 4ull * ntiles + 4ull * T;
-            d[0] = ts0; d[1] = ts1; d[2] = ts2; d[3] = __builtin_amdgcn_s_memtime();
+        __syncthreads();   // s_ticket, s_gin/s_tfn[slot], s_C/s_O, s_wfn reuse
+        if (p.debug && tid == 0 && Tp < ntiles) {
+            uint64_t* d = p.debug + 4ull * ntiles + 4ull * Tp;
+            d[0] = ts0; d[1] = ts1; d[2] = __builtin_amdgcn_s_memtime(); d[3] = spins;
         }
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+#pragma unroll
+            for (int h = 0; h < 8; ++h) vp[j][h] = vc[j][h];
+            mvp[j] = mvc[j]; lwp[j] = lwc[j]; exq[j] = exc[j];
+        }
+        Tp = T;
         T = Tn;
-        Tn = uni(s_ticket[0]);
-        __syncthreads();   // s_ticket / s_gin / s_C / s_wfn reuse in the next iteration
+        Tn = uni(s_ticket);
+        slot ^= 1u;
     }
 }
 

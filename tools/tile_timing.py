@@ -29,7 +29,7 @@ def main():
     wsb = s.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     ntiles = (n + TILE - 1) // TILE
-    dbg = torch.zeros(8 * ntiles, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(12 * ntiles, dtype=torch.int64, device="cuda")
     L = blt_amd._lib.lib()
     L.blt_debug_set_tile_record.argtypes = [ctypes.c_void_p]
     sp = torch.cuda.current_stream().cuda_stream
@@ -39,18 +39,17 @@ def main():
     L.blt_debug_set_tile_record(None)
     rec = dbg.cpu().numpy().astype(np.int64)
     how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
-    st = rec[4 * ntiles:].reshape(ntiles, 4)
-    p1, p2, p3 = st[:, 1] - st[:, 0], st[:, 2] - st[:, 1], st[:, 3] - st[:, 2]
-    tot = st[:, 3] - st[:, 0]
-    for name, v in (("phase1", p1), ("phase2", p2), ("phase3", p3), ("tile", tot)):
-        print(f"{name:7s} mean {v.mean():9.0f}  median {np.median(v):9.0f}  p90 {np.percentile(v, 90):9.0f} cycles")
-    f = how & 0xFF
-    win = how >> 8
+    st = rec[4 * ntiles:8 * ntiles].reshape(ntiles, 4)
+    ok = st[:, 0] != 0
+    p1, p2 = st[ok, 1] - st[ok, 0], st[ok, 2] - st[ok, 1]
+    for name, v in (("phase1+lookback", p1), ("resolve+emit", p2), ("iteration", p1 + p2)):
+        print(f"{name:16s} mean {v.mean():9.0f}  median {np.median(v):9.0f}  p90 {np.percentile(v, 90):9.0f} cycles")
+    sp = st[ok, 3]
+    print(f"look-back spins mean {sp.mean():.2f} median {np.median(sp)} p90 {np.percentile(sp, 90)} max {sp.max()}")
     valid = how != 0xFFFF
-    print("look-back: first-inclusive lane mean %.1f, windows mean %.2f max %d" %
-          (f[valid].mean(), (win[valid] / 64 + 1).mean(), (win[valid] // 64 + 1).max()))
-    span = st[:, 3].max() - st[:, 0].min()
-    print(f"kernel span {span} cycles; tiles per CU ~{ntiles / 256:.0f}")
+    f, qs, rounds = how & 63, (how >> 6) & 3, how >> 8
+    print("look-back: first-inclusive lane mean %.1f, window mean %.2f, extra rounds mean %.3f max %d" %
+          (f[valid].mean(), qs[valid].mean(), rounds[valid].mean(), rounds[valid].max()))
 
 
 if __name__ == "__main__":
