@@ -533,6 +533,30 @@ __device__ __forceinline__ uint32_t pk_nz(uint32_t v) {
     return r;
 }
 
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// LDS byte address of a __shared__ object.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const lds_u8*)(p);
+}
+// LDS byte addresses of the u16 entries at the low / high 16-bit index of t: base + 2 idx,
+// one v_mad_u32_u16 each (op_sel picks the high half).
+__device__ __forceinline__ uint32_t tab_addr_lo(uint32_t t, uint32_t base) {
+    uint32_t a;
+    asm("v_mad_u32_u16 %0, %1, 2, %2" : "=v"(a) : "v"(t), "s"(base));
+    return a;
+}
+__device__ __forceinline__ uint32_t tab_addr_hi(uint32_t t, uint32_t base) {
+    uint32_t a;
+    asm("v_mad_u32_u16 %0, %1, 2, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(t), "s"(base));
+    return a;
+}
+// (No ds_read_u16_d16_hi here: with SRAM-ECC on, gfx950 d16 loads zero the other half.)
+// a += 2 * bit, kept as one v_lshl_add (the compiler would re-derive each address from a count).
+__device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
+    asm("v_lshl_add_u32 %0, %1, 1, %0" : "+v"(a) : "v"(bit));
+}
+
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kS = 4;                                  // sub-tiles per tile
@@ -606,7 +630,7 @@ __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int i) {
 
 // ---- phase 1 of one sub-tile: lookups, lane function, wave function --------------------------
 template <bool kBE>
-__device__ __forceinline__ void phase1_sub(const uint16_t* s_tab, const uint32_t (&x)[4], uint32_t nxt,
+__device__ __forceinline__ void phase1_sub(uint32_t tab, const uint32_t (&x)[4], uint32_t nxt,
                                            uint64_t wb, uint64_t n, uint64_t bnext, int lane, uint32_t (&vals)[8],
                                            uint32_t& mv, uint32_t& lw, uint32_t& ex, uint32_t* wfn) {
     const uint32_t lo16 = 16u * (uint32_t)lane;
@@ -615,18 +639,23 @@ __device__ __forceinline__ void phase1_sub(const uint16_t* s_tab, const uint32_t
     // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63 keeps the
     // "old" operand, the byte after the wave's range
     const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false) & 0xFFu;
-    uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
+    uint32_t t0[8];
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
         // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
         const uint32_t lo = x[h >> 1], hi = (h >> 1) < 3 ? x[(h >> 1) + 1] : nb;
-        const uint32_t t0 = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
-        const uint32_t t = t0 ^ ((t0 >> 7) & 0x00FE00FEu);            // bank swizzle of b
-        const uint32_t v = (uint32_t)s_tab[t & 0xFFFFu] | ((uint32_t)s_tab[t >> 16] << 16);
-        vals[h] = v;
+        t0[h] = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
+        const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
+        const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
+        const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
+        vals[h] = va | (vb << 16);
+    }
+    uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
         // token of a itself, in output byte order: BE (a << 8), native a
-        const uint32_t self = kBE ? (t0 & 0xFF00FF00u) : ((t0 >> 8) & 0x00FF00FFu);
-        m32 |= pk_nz(v ^ self) << (2 * h);
+        const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
+        m32 |= pk_nz(vals[h] ^ self) << (2 * h);
     }
     uint32_t m = (m32 & 0xFFFFu) | (m32 >> 15);
     // valid positions, right neighbours inside the buffer, chunk ends
@@ -835,16 +864,15 @@ __device__ __forceinline__ void emit_sub(const PassParams& p, uint32_t Tp, uint3
     const uint64_t gb = 2ull * og;
     const uint64_t ab = gb & ~15ull;
     const uint32_t rg = (uint32_t)(gb - ab);
-    uint16_t* st16 = reinterpret_cast<uint16_t*>(st);
-    uint32_t a = rg + 2u * lane_off;                     // stage byte of this lane's next token
+    const uint16_t* st16 = reinterpret_cast<const uint16_t*>(st);
+    uint32_t a = lds_addr(st) + rg + 2u * lane_off;     // LDS byte address of this lane's next token
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
-        const uint32_t k = 2u * (uint32_t)h;
         const uint32_t tok = vals[h];
-        st16[a >> 1] = (uint16_t)tok;
-        a += 2u * ((L >> k) & 1u);
-        if (h < 7 || ((L >> 15) & 1u)) st16[a >> 1] = (uint16_t)(tok >> 16);
-        a += 2u * ((L >> (k + 1)) & 1u);
+        *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
+        add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+        if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
+        if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
     }
     // token index of a chunk start in this lane's segment
     while (cnext < wb) cnext += cs;
@@ -904,6 +932,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
     }
     __syncthreads();
+    const uint32_t tab = uni(lds_addr(s_tab));
     uint32_t T = uni(s_wfn[0][0]);    // tile in phase 1
     uint32_t Tn = uni(s_wfn[0][1]);   // tile whose bytes are loaded during this iteration's emission
     uint32_t Tp = kNone;              // tile waiting for emission
@@ -942,7 +971,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             for (int j = 0; j < kS; ++j) {
                 const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
                 while (bnext <= wb) bnext += cs;
-                phase1_sub<kBE>(s_tab, x[j], nxt[j], wb, n, bnext, lane, vc[j], mvc[j], lwc[j], exc[j],
+                phase1_sub<kBE>(tab, x[j], nxt[j], wb, n, bnext, lane, vc[j], mvc[j], lwc[j], exc[j],
                                 s_wfn[(uint32_t)j * kWaves + wave]);
             }
         }

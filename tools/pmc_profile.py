@@ -18,6 +18,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GIB = 1 << 30
+CHUNK = 16 << 20   # bench.py's --chunksize
 
 GROUPS = {
     "time": ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
@@ -74,6 +76,15 @@ def main():
     if "FETCH_SIZE" in pd and "WRITE_SIZE" in pd:
         result["hbm_bytes_per_launch"] = int((2.0 * pd["FETCH_SIZE"] + pd["WRITE_SIZE"]) * 1024)
         result["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 FETCH_SIZE counts half of wide reads"
+        # what bench.py reports as roofline.traffic for the same workload
+        n = GIB
+        for i, x in enumerate(bench_args):
+            if x == "--bytes-per-gpu":
+                n = int(bench_args[i + 1])
+        with open(os.path.join(a.outdir, "traffic.json"), "w") as f:
+            json.dump({"bytes_per_gpu": n, "chunk_size": CHUNK, "kernel": a.kernel,
+                       "hbm_bytes_per_launch": result["hbm_bytes_per_launch"], "note": result["traffic_note"]}, f,
+                      indent=1)
     with open(os.path.join(a.outdir, "pmc_summary.json"), "w") as f:
         json.dump(result, f, indent=1, sort_keys=True)
     print(json.dumps(result, indent=1, sort_keys=True))
