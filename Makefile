@@ -37,3 +37,13 @@ clean:
 	rm -rf $(OBJDIR) $(LIB) $(SYNTH) $(ORACLE)
 
 .PHONY: all clean
+
+# Timing experiments (tools/tile_timing.py with BLT_LIB_PATH): kernel variants with parts of
+# the work removed.  Wrong output by construction; never used by the product or the tests.
+EXPS := 1 2 4 6 7
+exp: $(foreach e,$(EXPS),build/exp/libblt_bpe_exp$(e).so)
+build/exp/libblt_bpe_exp%.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
+	mkdir -p build/exp
+	$(HIPCC) $(HIPFLAGS) -DBLT_EXP=$* -c $< -o build/exp/k$*.o
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/exp/k$*.o $(OBJDIR)/blt_host.o -lpthread
+.PHONY: exp

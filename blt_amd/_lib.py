@@ -10,7 +10,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libblt_bpe.so")
+# BLT_LIB_PATH: an alternative build of the same library (tools/ timing experiments only).
+LIB_PATH = os.environ.get("BLT_LIB_PATH") or os.path.join(_HERE, "libblt_bpe.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "blt_bpe.h")
 
 BLT_E_NOT_FOUND = -2

@@ -397,6 +397,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.dense = columnar ? (be ? t->self_be : t->self_ne) : t->dense;
     p.hslots = t->hslots;
     p.hmask = h->hmask;
+    p.cs_magic = cs ? ~0ull / cs : 0;
     p.debug = g_debug_tiles;
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));

@@ -31,6 +31,7 @@ struct PassParams {
                                // self-token table (absent (a, b) -> a) in the output byte order
     const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
     uint64_t hmask;
+    uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins

@@ -628,83 +628,144 @@ __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int i) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
 }
 
-// ---- phase 1 of one sub-tile: lookups, lane function, wave function --------------------------
+// Phase-1 state of one tile, per lane.
+struct TileState {
+    uint32_t v[kS][8];   // looked-up tokens, two per register
+    uint32_t mv[kS];     // merge mask | valid mask << 16
+    uint32_t lw[kS];     // carry-in for wave carry-in 0 | for wave carry-in 1 << 1
+    uint32_t ex[kS];     // exclusive prefix count, carry-in 0 | carry-in 1 << 16
+};
+
+// ---- per-tile scalars ---------------------------------------------------------------------
+struct TInfo {
+    uint32_t rn;    // positions left in the buffer from the tile start (clamped to 2^31 - 1)
+    uint32_t bge;   // first chunk start >= the tile start, relative (clamped to 2^16)
+    uint64_t k0;    // its chunk index
+};
+
+// x / cs by a high multiply with the host's reciprocal (at most two corrections).
+__device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
+    TInfo t;
+    const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
+    const uint64_t left = p.n > tile0 ? p.n - tile0 : 0;
+    t.rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+    uint64_t q = __umul64hi(tile0, p.cs_magic);
+    uint64_t r = tile0 - q * p.cs;
+    if (r >= p.cs) { q += 1; r -= p.cs; }
+    if (r >= p.cs) { q += 1; r -= p.cs; }
+    const uint64_t d = r ? p.cs - r : 0;
+    t.bge = (uint32_t)(d > 0x10000ull ? 0x10000ull : d);
+    t.k0 = q + (r ? 1u : 0u);
+    return t;
+}
+
+// ---- phase 1 of a tile: lookups, lane functions, wave functions ------------------------------
+// Three straight-line passes over the kS sub-tiles (lookups; the rare uniform fix-up of buffer
+// and chunk ends; lane functions and wave resolves), so the scheduler can overlap sub-tiles.
 template <bool kBE>
-__device__ __forceinline__ void phase1_sub(uint32_t tab, const uint32_t (&x)[4], uint32_t nxt,
-                                           uint64_t wb, uint64_t n, uint64_t bnext, int lane, uint32_t (&vals)[8],
-                                           uint32_t& mv, uint32_t& lw, uint32_t& ex, uint32_t* wfn) {
-    const uint32_t lo16 = 16u * (uint32_t)lane;
-    // positions left in the buffer from this wave's first one (clamped: uniform 32-bit)
-    const uint32_t rem = wb >= n ? 0u : (n - wb > 2u * kWavePos ? 2u * kWavePos : (uint32_t)(n - wb));
-    // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63 keeps the
-    // "old" operand, the byte after the wave's range
-    const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false) & 0xFFu;
-    uint32_t t0[8];
+__device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS][4], const uint32_t (&nxt)[kS],
+                                            const TInfo& ti, uint32_t cs32, uint32_t wave, int lane,
+                                            TileState& st, uint32_t (*wfn)[4]) {
+    uint32_t m[kS];
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
-        const uint32_t lo = x[h >> 1], hi = (h >> 1) < 3 ? x[(h >> 1) + 1] : nb;
-        t0[h] = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
-        const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
-        const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
-        const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
-        vals[h] = va | (vb << 16);
-    }
-    uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        // token of a itself, in output byte order: BE (a << 8), native a
-        const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
-        m32 |= pk_nz(vals[h] ^ self) << (2 * h);
-    }
-    uint32_t m = (m32 & 0xFFFFu) | (m32 >> 15);
-    // valid positions, right neighbours inside the buffer, chunk ends
-    const int32_t r = (int32_t)rem - (int32_t)lo16;                   // positions left from mine
-    const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
-    m &= (vmask >> 1) | (r > 16 ? 0x8000u : 0u);
-    uint32_t forced = (r >= 1 && r <= 16) ? (1u << (r - 1)) : 0u;     // the buffer's last position
-    if (bnext < n && bnext - 1 - wb < kWavePos) {                     // chunk end b - 1 here
-        const uint32_t e = (uint32_t)(bnext - 1 - wb) - lo16;
-        if (e < 16u) { m &= ~(1u << e); forced |= 1u << e; }
-    }
-    if (__ballot(forced != 0)) {   // rare: a cut merge emits its raw byte
+    for (int j = 0; j < kS; ++j) {
+        // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63 keeps
+        // the "old" operand, the byte after the wave's range
+        const uint32_t nb =
+            (uint32_t)__builtin_amdgcn_update_dpp((int)nxt[j], (int)x[j][0], 0x130, 0xF, 0xF, false) & 0xFFu;
+        uint32_t t0[8];
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-            const uint32_t xw = x[h >> 1];
-            const uint32_t raw = __builtin_amdgcn_perm(xw, xw, kBE ? ((h & 1) ? 0x030C020Cu : 0x010C000Cu)
-                                                                   : ((h & 1) ? 0x0C030C02u : 0x0C010C00u));
-            const uint32_t fm = (((forced >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) |
-                                (((forced >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
-            vals[h] = (vals[h] & ~fm) | (raw & fm);
+            // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
+            const uint32_t lo = x[j][h >> 1], hi = (h >> 1) < 3 ? x[j][(h >> 1) + 1] : nb;
+            t0[h] = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
+            const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
+#if defined(BLT_EXP) && (BLT_EXP & 1)
+            st.v[j][h] = (t * 0x9E3779B1u) & 0xFF00FF00u;   // timing experiment: no LDS lookups
+#else
+            const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
+            const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
+            st.v[j][h] = va | (vb << 16);
+#endif
+        }
+        uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            // token of a itself, in output byte order: BE (a << 8), native a
+            const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
+            m32 |= pk_nz(st.v[j][h] ^ self) << (2 * h);
+        }
+        m[j] = (m32 & 0xFFFFu) | (m32 >> 15);
+    }
+    // buffer end and chunk ends (uniform per wave range; rare)
+    uint32_t bnext = ti.bge;   // first chunk start > the wave range's first position
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
+        bnext = bnext <= wrel ? bnext + cs32 : bnext;
+        bnext = bnext <= wrel ? bnext + cs32 : bnext;
+        const uint32_t rem = ti.rn > wrel ? ti.rn - wrel : 0u;
+        const bool has_end = bnext - 1u - wrel < kWavePos;
+        if (rem <= kWavePos || has_end) {
+            const int32_t r = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
+            const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
+            uint32_t mm = m[j] & ((vmask >> 1) | (r > 16 ? 0x8000u : 0u));
+            uint32_t forced = (r >= 1 && r <= 16) ? (1u << (r - 1)) : 0u;   // the buffer's last position
+            if (has_end) {                                                   // chunk end b - 1 here
+                const uint32_t e = bnext - 1u - wrel - 16u * (uint32_t)lane;
+                if (e < 16u) { mm &= ~(1u << e); forced |= 1u << e; }
+            }
+            if (__ballot(forced != 0)) {   // a cut merge emits its raw byte
+#pragma unroll
+                for (int h = 0; h < 8; ++h) {
+                    const uint32_t xw = x[j][h >> 1];
+                    const uint32_t raw = __builtin_amdgcn_perm(xw, xw, kBE ? ((h & 1) ? 0x030C020Cu : 0x010C000Cu)
+                                                                           : ((h & 1) ? 0x0C030C02u : 0x0C010C00u));
+                    const uint32_t fm = (((forced >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) |
+                                        (((forced >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
+                    st.v[j][h] = (st.v[j][h] & ~fm) | (raw & fm);
+                }
+            }
+            m[j] = mm;
+            st.mv[j] = mm | (vmask << 16);
+        } else {
+            st.mv[j] = m[j] | 0xFFFF0000u;
         }
     }
-    mv = m | (vmask << 16);
-    // lane function, both carry-in hypotheses: low half c = 0 (position 0 consumed), high
-    // half c = 1 (merges_for, packed 16-bit)
-    const uint32_t mc = (m & ~1u) | (m << 16);
-    const uint32_t st = mc & ~pk_shl1(mc);
-    const uint32_t rodd = mc & ~pk_add(mc, st & 0xAAAAAAAAu);
-    const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
-    const uint32_t L = ~(pk_shl1(M) | 1u) & (vmask | (vmask << 16));
-    const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
-    const uint32_t cout = ((M >> 31) & 1u) ^ 1u;                     // carry-out if not identity
-    const uint32_t ident = m == 0xFFFFu;
-    // wave resolve
-    const uint64_t nonid = __ballot(!ident);
-    const uint64_t cmask = __ballot(cout);
-    const uint64_t below = nonid & ((1ull << lane) - 1ull);
-    const uint32_t hb = below != 0;
-    const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
-    const uint32_t c0 = hb ? bc : 0u, c1 = hb ? bc : 1u;
-    const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
-    const uint32_t incl = wave_scan(packed);
-    ex = incl - packed;
-    lw = hb | (bc << 1);
-    if (lane == 63) {
-        wfn[0] = nonid == 0;
-        wfn[1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
-        wfn[2] = incl & 0xFFFFu;
-        wfn[3] = incl >> 16;
+    // lane functions (both carry-in hypotheses, packed 16-bit) and wave resolves
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        const uint32_t vm = st.mv[j] >> 16;
+        const uint32_t mc = (m[j] & ~1u) | (m[j] << 16);
+        const uint32_t sst = mc & ~pk_shl1(mc);
+        const uint32_t rodd = mc & ~pk_add(mc, sst & 0xAAAAAAAAu);
+        const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
+        const uint32_t L = ~(pk_shl1(M) | 1u) & (vm | (vm << 16));
+        const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
+        // Carries across the wave, on SGPR masks: a lane's carry-in is the carry-out of the
+        // nearest non-identity lane below it (an identity lane merges all 16 positions), or
+        // the wave's carry-in c.  Y = lanes fed carry 1 by such a lane: each D = (non-identity,
+        // carry-out 1) lane's carry runs up through the identity lanes above it and stops at
+        // the next non-identity lane, i.e. the carry chain of M + (D << 1); F = lanes at or below
+        // the lowest non-identity lane, fed by c.
+        const uint64_t nonid = __ballot(m[j] != 0xFFFFu);
+        const uint64_t cmask = __ballot(((M >> 31) & 1u) == 0u);   // carry-out 1 (if not identity)
+        const uint64_t D = cmask & nonid, Mi = ~nonid, A = D << 1;
+        const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
+        const uint64_t F = nonid ? ((nonid & (0ull - nonid)) << 1) - 1ull : ~0ull;
+        const uint64_t CI0 = Y, CI1 = Y | F;
+        const uint32_t c0 = (uint32_t)(CI0 >> lane) & 1u, c1 = (uint32_t)(CI1 >> lane) & 1u;
+        const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
+        const uint32_t incl = wave_scan(packed);
+        st.ex[j] = incl - packed;
+        st.lw[j] = c0 | (c1 << 1);   // this lane's carry-in for wave carry-in 0 | 1
+        if (lane == 63) {
+            const uint32_t g = (uint32_t)j * kWaves + wave;
+            wfn[g][0] = nonid == 0;
+            wfn[g][1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
+            wfn[g][2] = incl & 0xFFFFu;
+            wfn[g][3] = incl >> 16;
+        }
     }
 }
 
@@ -844,62 +905,108 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
     }
 }
 
-// ---- emission of one sub-tile of the pending tile -------------------------------------------
-__device__ __forceinline__ void emit_sub(const PassParams& p, uint32_t Tp, uint32_t j, uint32_t wave, int lane,
-                                         const uint32_t (&vals)[8], uint32_t mv, uint32_t lw, uint32_t ex,
-                                         const uint32_t* gin, uint32_t C, uint64_t O, uint64_t wb, uint64_t& cnext,
-                                         uint8_t* st, uint8_t* out) {
-    const uint64_t n = p.n, cs = p.cs;
-    const uint32_t cg = uni(gin[C]);
-    const uint64_t og = O + uni(gin[2 + C]);                 // wave's first token
-    const uint32_t m = mv & 0xFFFFu, vmask = mv >> 16;
-    const uint32_t c = (lw & 1u) ? (lw >> 1) : cg;
-    const uint32_t lane_off = cg ? (ex >> 16) : (ex & 0xFFFFu);
-    const uint32_t mc = c ? m : (m & ~1u);
-    const uint32_t sst = mc & ~(mc << 1);
-    const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
-    const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
-    const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
-    const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
-    const uint64_t gb = 2ull * og;
-    const uint64_t ab = gb & ~15ull;
-    const uint32_t rg = (uint32_t)(gb - ab);
-    const uint16_t* st16 = reinterpret_cast<const uint16_t*>(st);
-    uint32_t a = lds_addr(st) + rg + 2u * lane_off;     // LDS byte address of this lane's next token
+// ---- emission of the pending tile --------------------------------------------------------
+// Tile-level: carry-in C, O tokens before the tile; the output resource starts at the 16-byte
+// boundary at or below byte 2 O, so every offset below is 32-bit.
+__device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, const TInfo& ti, uint32_t cs32,
+                                          uint32_t wave, int lane, const TileState& st, const uint32_t (*gin)[4],
+                                          uint32_t C, uint64_t O, uint8_t* stg) {
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+    const uint64_t obase = (2ull * O) & ~15ull;
+    const uint32_t orel = (uint32_t)(2ull * O - obase);
+    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
+    const uint16_t* st16 = reinterpret_cast<const uint16_t*>(stg);
+    const uint32_t stg_lds = lds_addr(stg);
+    uint32_t cnext = ti.bge;   // first chunk start >= the wave range's first position
+    uint64_t kc = ti.k0;       // its chunk index
 #pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        const uint32_t tok = vals[h];
-        *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
-        add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
-        if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
-        if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+    for (int j = 0; j < kS; ++j) {
+        const uint32_t g = (uint32_t)j * kWaves + wave;
+        const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
+        const uint32_t cg = uni(gin[g][C]);
+        const uint32_t goff = uni(gin[g][2 + C]);          // tokens before this wave range in the tile
+        const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
+        const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
+        const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
+        const uint32_t mc = c ? m : (m & ~1u);
+        const uint32_t sst = mc & ~(mc << 1);
+        const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
+        const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+        const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
+        const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
+        const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
+        const uint32_t ab = gb & ~15u, rg = gb - ab;
+        uint32_t a = stg_lds + rg + 2u * lane_off;          // LDS byte address of this lane's next token
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const uint32_t tok = st.v[j][h];
+#if defined(BLT_EXP) && (BLT_EXP & 2)
+            asm volatile("" :: "v"(tok), "v"(a));           // timing experiment: no stage stores
+            add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+            if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+#else
+            *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
+            add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+            if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
+            if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+#endif
+        }
+        // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
+        if (cnext < wrel) { cnext += cs32; ++kc; }
+        if (cnext < wrel) { cnext += cs32; ++kc; }
+        if (p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos) {
+            const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
+            if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+        }
+        // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each,
+        // lanes 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order queue).
+        const uint32_t re = rg + 2u * wcnt;
+        const uint32_t hend = ((rg + 15u) & ~15u) < re ? ((rg + 15u) & ~15u) : re;
+        const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
+        const uint32_t nfull = (tbeg - hend) >> 4;
+#if defined(BLT_EXP) && (BLT_EXP & 4)
+        if (nfull == 12345u)   // timing experiment: no copy-out
+#endif
+        for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
+            const uint32_t o = hend + 16u * i;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + o);
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)(ab + o), 0, 0);
+        }
+        if (lane < 16) {
+            const uint32_t o = lane < 8 ? rg + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+            const uint32_t lim = lane < 8 ? hend : re;
+            if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)(ab + o), 0, 0);
+        }
     }
-    // token index of a chunk start in this lane's segment
-    while (cnext < wb) cnext += cs;
-    if (p.chunk_off && cnext < n && cnext - wb < kWavePos) {
-        const uint32_t e = (uint32_t)(cnext - wb) - 16u * (uint32_t)lane;
-        if (e < 16u) p.chunk_off[cnext / cs] = og + lane_off + __popc(L & ((1u << e) - 1u));
-    }
-    // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each, lanes
-    // 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order LDS queue).
-    const uint32_t re = rg + 2u * wcnt;
-    if (ab + re > p.out_cap) {
-        if (lane == 0) record_error(p, 2u, Tp, j, O, ab + re, C);
-        return;
-    }
-    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + ab, p.out_cap - ab);
-    const uint32_t hend = ((rg + 15u) & ~15u) < re ? ((rg + 15u) & ~15u) : re;
-    const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
-    const uint32_t nfull = (tbeg - hend) >> 4;
-    for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
-        const uint32_t o = hend + 16u * i;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(st + o);
-        __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)o, 0, 0);
-    }
-    if (lane < 16) {
-        const uint32_t o = lane < 8 ? rg + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
-        const uint32_t lim = lane < 8 ? hend : re;
-        if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)o, 0, 0);
+}
+
+// ---- refill: the bytes of tile Tn into x --------------------------------------------------
+__device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint32_t wave, int lane,
+                                          uint32_t (&x)[kS][4], uint32_t (&nxt)[kS]) {
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+    const uint64_t tile0 = (uint64_t)Tn * kTilePosBytes;
+    const uint64_t left = p.n > tile0 ? p.n - tile0 : 0;
+    const __amdgpu_buffer_rsrc_t r = rsrc_at(in + tile0, left);
+    const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
+        if (wrel + kWavePos <= rn) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, (int)wrel, 0);
+            x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
+        } else {   // the buffer's last wave range: checked bytes (past the end read as 0)
+            // the range check covers voffset only, never soffset: the offset goes in voffset
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t d = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    d |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)wrel + 16 * lane + 4 * q + b, 0, 0)
+                         << (8 * b);
+                x[j][q] = d;
+            }
+        }
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(wrel + kWavePos), 0, 0);
     }
 }
 
@@ -917,10 +1024,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = uni((uint32_t)tid >> 6);
-    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
-    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
-    const uint64_t n = p.n, cs = p.cs;
+    const uint64_t n = p.n;
     const uint32_t ntiles = p.ntiles;
+    const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
     if (tid == 0) {
         s_wfn[0][0] = atomicAdd(p.ctl, 1u);
@@ -939,16 +1045,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __syncthreads();
 
     uint32_t x[kS][4];      // input bytes of each sub-tile of T
-    uint32_t nxt[kS];       // byte after this wave's range (lane 63's right neighbour)
-    if (T < ntiles) {
-#pragma unroll
-        for (int j = 0; j < kS; ++j) {
-            const uint64_t wb = (uint64_t)T * kTilePosBytes + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-            load_sub(rsrc(in, wb, n), wb + kWavePos <= n, lane, x[j], nxt[j]);
-        }
-    }
-    uint32_t vp[kS][8], mvp[kS], lwp[kS], exq[kS];   // phase-1 state of Tp
-    uint32_t slot = 0;                               // s_gin / s_tfn slot of T (Tp has slot ^ 1)
+    uint32_t nxt[kS];       // byte after each wave range (lane 63's right neighbour)
+    if (T < ntiles) load_tile(p, T, wave, lane, x, nxt);
+    TInfo ti = {}, tip = {};
+    if (T < ntiles) ti = tile_info(p, T);
+    TileState sp, sc;       // phase-1 state of Tp (pending) and of T (current)
+    uint32_t slot = 0;      // s_gin / s_tfn slot of T (Tp has slot ^ 1)
 
     while (T < ntiles || Tp < ntiles) {
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
@@ -961,20 +1063,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (tid == 64 && Tn < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
-        // ---- phase 1 of T -------------------------------------------------------------------
-        uint32_t vc[kS][8], mvc[kS], lwc[kS], exc[kS];
-        if (T < ntiles) {
-            const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
-            // first chunk start > this wave's first position; advanced monotonically
-            uint64_t bnext = uni64(((tile0 + (uint64_t)wave * kWavePos) / cs + 1) * cs);
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-                const uint64_t wb = tile0 + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-                while (bnext <= wb) bnext += cs;
-                phase1_sub<kBE>(tab, x[j], nxt[j], wb, n, bnext, lane, vc[j], mvc[j], lwc[j], exc[j],
-                                s_wfn[(uint32_t)j * kWaves + wave]);
-            }
-        }
+        // ---- phase 1 of T ---------------------------------------------------------------------
+        if (T < ntiles) phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn);
 
         // ---- carry-in and offset of Tp (wave 0) --------------------------------------------
         uint32_t spins = 0;
@@ -984,12 +1074,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
             if (lane == 0) {
                 const uint32_t* tf = s_tfn[slot ^ 1u];
-                const uint64_t tot = C ? tf[3] : tf[2];
-                const uint64_t end = O + tot;
+                const uint64_t end = O + (C ? tf[3] : tf[2]);
                 if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
                     record_error(p, 4u, Tp, 0xFFu, O, end, C);
                     O = 0; C = 1;
                 }
+                if (2ull * (O + (C ? tf[3] : tf[2])) > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, end, C);
                 if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf[1] : tf[0], O + (C ? tf[3] : tf[2])));
                 s_C = C;
                 s_O = O;
@@ -1013,38 +1103,18 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- resolve and publish T (last wave) ----------------------------------------------
         if (wave == kWaves - 1 && T < ntiles) resolve_tile(p, T, lane, s_wfn, s_gin[slot], s_tfn[slot]);
 
-        // ---- emit Tp; refill registers with Tn ---------------------------------------------
-        {
-            const uint32_t C = uni(s_C);
-            const uint64_t O = uni64(s_O);
-            const uint64_t tile0p = (uint64_t)(Tp < ntiles ? Tp : 0) * kTilePosBytes;
-            uint64_t cnext = 0;
-            if (Tp < ntiles) cnext = uni64(((tile0p + (uint64_t)wave * kWavePos + cs - 1) / cs) * cs);
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-                const uint32_t g = (uint32_t)j * kWaves + wave;
-                if (Tp < ntiles) {
-                    const uint64_t wb = tile0p + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-                    emit_sub(p, Tp, (uint32_t)j, wave, lane, vp[j], mvp[j], lwp[j], exq[j], s_gin[slot ^ 1u][g], C, O,
-                             wb, cnext, s_stage[wave], out);
-                }
-                if (Tn < ntiles) {
-                    const uint64_t nb2 = (uint64_t)Tn * kTilePosBytes + (uint64_t)j * kSubPos + (uint64_t)wave * kWavePos;
-                    load_sub(rsrc(in, nb2, n), nb2 + kWavePos <= n, lane, x[j], nxt[j]);
-                }
-            }
-        }
+        // ---- emit Tp; load Tn's bytes -------------------------------------------------------
+        if (Tp < ntiles) emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[slot ^ 1u], uni(s_C), uni64(s_O),
+                                   s_stage[wave]);
+        if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
         __syncthreads();   // s_ticket, s_gin/s_tfn[slot], s_C/s_O, s_wfn reuse
         if (p.debug && tid == 0 && Tp < ntiles) {
             uint64_t* d = p.debug + 4ull * ntiles + 4ull * Tp;
             d[0] = ts0; d[1] = ts1; d[2] = __builtin_amdgcn_s_memtime(); d[3] = spins;
         }
-#pragma unroll
-        for (int j = 0; j < kS; ++j) {
-#pragma unroll
-            for (int h = 0; h < 8; ++h) vp[j][h] = vc[j][h];
-            mvp[j] = mvc[j]; lwp[j] = lwc[j]; exq[j] = exc[j];
-        }
+        sp = sc;
+        tip = ti;
+        if (Tn < ntiles) ti = tile_info(p, Tn);
         Tp = T;
         T = Tn;
         Tn = uni(s_ticket);
