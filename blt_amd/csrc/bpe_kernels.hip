@@ -557,13 +557,16 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
     asm("v_lshl_add_u32 %0, %1, 1, %0" : "+v"(a) : "v"(bit));
 }
 
-constexpr int kThreads = 512;
+constexpr int kThreads = 1024;                         // 16 waves: 4 per SIMD hide LDS and VALU latency
 constexpr int kWaves = kThreads / 64;
-constexpr int kS = 4;                                  // sub-tiles per tile
+constexpr int kS = 2;                                  // sub-tiles per tile
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
-constexpr int kStageWave = 2 * (int)kWavePos + 32;     // tokens + 16-byte alignment slack
+// Per-wave token stage: a wave range of 1024 positions emits 512..1024 tokens; the stage holds
+// 521 (2-byte aligned start + up to 1042 bytes) — every range of a text whose pairs mostly merge.
+// A range with more tokens stores them straight to global memory (emit_direct).
+constexpr int kStageWave = 1056;
 constexpr int kLbWin = 4;                              // look-back windows of 64 per round trip
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
@@ -571,6 +574,7 @@ static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
 static_assert(kGroups <= 64, "one lane per group in the tile resolve");
 static_assert(kStageWave % 16 == 0, "stage alignment");
+static_assert((uint64_t)kS * kSubPos == kTilePosBytes, "tile = kS sub-tiles");
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
@@ -702,8 +706,7 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
-        bnext = bnext <= wrel ? bnext + cs32 : bnext;
-        bnext = bnext <= wrel ? bnext + cs32 : bnext;
+        while (bnext <= wrel) bnext += cs32;   // uniform; kSubPos / 4096 steps at most
         const uint32_t rem = ti.rn > wrel ? ti.rn - wrel : 0u;
         const bool has_end = bnext - 1u - wrel < kWavePos;
         if (rem <= kWavePos || has_end) {
@@ -936,6 +939,24 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
         const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
         const uint32_t ab = gb & ~15u, rg = gb - ab;
+        // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
+        while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
+        if (p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos) {
+            const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
+            if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+        }
+        if (rg + 2u * wcnt > (uint32_t)kStageWave) {
+            // rare (few merges): each landed token straight to global memory
+            uint32_t o = gb + 2u * lane_off;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if ((L >> k) & 1u) {
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(st.v[j][k >> 1] >> (16 * (k & 1))), ro, (int)o, 0, 0);
+                    o += 2u;
+                }
+            }
+            continue;
+        }
         uint32_t a = stg_lds + rg + 2u * lane_off;          // LDS byte address of this lane's next token
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
@@ -950,13 +971,6 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
             if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
 #endif
-        }
-        // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
-        if (cnext < wrel) { cnext += cs32; ++kc; }
-        if (cnext < wrel) { cnext += cs32; ++kc; }
-        if (p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos) {
-            const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
-            if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
         // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each,
         // lanes 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order queue).
@@ -1097,6 +1111,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             }
         }
         if (tid == 64) s_ticket = tk;
+        const uint64_t tw0 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
         __syncthreads();
         const uint64_t ts1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
 
@@ -1107,7 +1122,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (Tp < ntiles) emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[slot ^ 1u], uni(s_C), uni64(s_O),
                                    s_stage[wave]);
         if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
+        const uint64_t tw1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
         __syncthreads();   // s_ticket, s_gin/s_tfn[slot], s_C/s_O, s_wfn reuse
+        if (p.debug && T < ntiles && lane == 0) {
+            // per wave: phase-1 work, first-barrier wait, emission work, second-barrier wait
+            const uint64_t tw2 = __builtin_amdgcn_s_memtime();
+            uint64_t* w = p.debug + 8ull * ntiles + 4ull * ((uint64_t)T * kWaves + wave);
+            w[0] = tw0 - ts0; w[1] = ts1 - tw0; w[2] = tw1 - ts1; w[3] = tw2 - tw1;
+        }
         if (p.debug && tid == 0 && Tp < ntiles) {
             uint64_t* d = p.debug + 4ull * ntiles + 4ull * Tp;
             d[0] = ts0; d[1] = ts1; d[2] = __builtin_amdgcn_s_memtime(); d[3] = spins;

@@ -1,6 +1,6 @@
 """Collects rocprofv3 PMC counters for the merge-scan kernel, one counter group per pass.
 
-    python tools/pmc_profile.py OUTDIR [--groups A,B,...] [-- bench args]
+    python tools/pmc_profile.py OUTDIR [--groups A,B,...] [--kernel NAME] [-- bench args]
 
 Each group runs `rocprofv3 --pmc <counters> --kernel-trace --output-format csv -- python
 bench.py ...` as a child process (counters in their own passes, never with sys/runtime
@@ -63,9 +63,13 @@ def main():
     ap.add_argument("outdir")
     ap.add_argument("--groups", default=",".join(GROUPS))
     ap.add_argument("--kernel", default="scan_bytes_kernel")
-    ap.add_argument("bench_args", nargs=argparse.REMAINDER)
-    a = ap.parse_args()
-    bench_args = [x for x in a.bench_args if x != "--"] or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline"]
+    argv = sys.argv[1:]
+    extra = []
+    if "--" in argv:
+        i = argv.index("--")
+        argv, extra = argv[:i], argv[i + 1:]
+    a = ap.parse_args(argv)
+    bench_args = extra or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline"]
     os.makedirs(a.outdir, exist_ok=True)
     result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}}
     for g in a.groups.split(","):

@@ -29,7 +29,7 @@ def main():
     wsb = s.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     ntiles = (n + TILE - 1) // TILE
-    dbg = torch.zeros(12 * ntiles, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros((8 + 4 * 16) * ntiles, dtype=torch.int64, device="cuda")
     L = blt_amd._lib.lib()
     L.blt_debug_set_tile_record.argtypes = [ctypes.c_void_p]
     sp = torch.cuda.current_stream().cuda_stream
@@ -46,6 +46,13 @@ def main():
         print(f"{name:16s} mean {v.mean():9.0f}  median {np.median(v):9.0f}  p90 {np.percentile(v, 90):9.0f} cycles")
     sp = st[ok, 3]
     print(f"look-back spins mean {sp.mean():.2f} median {np.median(sp)} p90 {np.percentile(sp, 90)} max {sp.max()}")
+    wv = rec[8 * ntiles:].reshape(ntiles, -1, 4)
+    okw = wv[:, 0, 0] > 0
+    wv = wv[okw]
+    print("per wave (mean cycles): phase1-work  B1-wait  emit-work  B2-wait")
+    for w in range(wv.shape[1]):
+        a = wv[:, w, :].mean(axis=0)
+        print(f"  wave {w:2d}: {a[0]:8.0f} {a[1]:8.0f} {a[2]:8.0f} {a[3]:8.0f}")
     valid = how != 0xFFFF
     f, qs, rounds = how & 63, (how >> 6) & 3, how >> 8
     print("look-back: first-inclusive lane mean %.1f, window mean %.2f, extra rounds mean %.3f max %d" %
