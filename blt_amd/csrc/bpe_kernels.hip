@@ -995,21 +995,34 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
 }
 
 // ---- refill: the bytes of tile Tn into x --------------------------------------------------
+// Straight-line 16-byte loads through a descriptor clamped to whole dwords (a load must not
+// reach past the buffer; a partly out-of-range load reads 0), then, only in the wave range
+// holding the buffer end, the lanes' bytes again one by one.  Keeping the common path free of
+// branches lets the loads land in x directly: a branch that merges x would make the compiler
+// wait for them right here.
 __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint32_t wave, int lane,
                                           uint32_t (&x)[kS][4], uint32_t (&nxt)[kS]) {
     const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
     const uint64_t tile0 = (uint64_t)Tn * kTilePosBytes;
     const uint64_t left = p.n > tile0 ? p.n - tile0 : 0;
     const __amdgpu_buffer_rsrc_t r = rsrc_at(in + tile0, left);
+    const __amdgpu_buffer_rsrc_t rd = rsrc_at(in + tile0, left & ~3ull);
     const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
-        if (wrel + kWavePos <= rn) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, (int)wrel, 0);
-            x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
-        } else {   // the buffer's last wave range: checked bytes (past the end read as 0)
-            // the range check covers voffset only, never soffset: the offset goes in voffset
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, 0);
+        x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
+        // the byte after the range, as its whole (4-aligned) dword: a u8 load would be masked
+        // right here, which makes the compiler wait for it.  The range check covers voffset
+        // only, never soffset: offsets go in voffset.
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(wrel + kWavePos), 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
+        if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
+            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(wrel + kWavePos), 0, 0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 uint32_t d = 0;
@@ -1020,7 +1033,32 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
                 x[j][q] = d;
             }
         }
-        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(wrel + kWavePos), 0, 0);
+    }
+}
+
+// Workgroup-internal dataflow: monotonic LDS counters instead of block barriers, so waves drift
+// (a fast wave starts the next phase while a slow one finishes) and phase-1 LDS reads, emission
+// LDS writes and VALU work of different waves overlap.  Every wait names exactly one producer
+// condition; rings of kRing slots cover the at most two iterations of drift the chain allows
+// (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
+constexpr int kRing = 4;
+constexpr uint32_t kWaitLimit = 1u << 22;
+
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
+    return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(uint32_t* f, uint32_t v) {
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Waits until *f >= v; on a (never expected) timeout flags error bit 8 and lets the wave go on.
+__device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, uint32_t v) {
+    uint32_t spins = 0;
+    while (lds_acquire(f) < v) {
+        if (++spins > kWaitLimit) {
+            if ((threadIdx.x & 63) == 0) atomicOr(p.ctl + 1, 8u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
@@ -1028,12 +1066,17 @@ template <bool kBE>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
-    __shared__ uint32_t s_wfn[kGroups][4];       // wave functions of the tile in phase 1
-    __shared__ uint32_t s_gin[2][kGroups][4];    // per slot: group carry-in |H=0,1, offset |H=0,1
-    __shared__ uint32_t s_tfn[2][4];             // per slot: tile co0, co1, tot0, tot1
-    __shared__ uint32_t s_C;
-    __shared__ uint64_t s_O;
-    __shared__ uint32_t s_ticket;
+    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroups][4];   // wave functions (phase 1)
+    __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
+    __shared__ uint32_t s_tfn[kRing][4];            // tile co0, co1, tot0, tot1
+    __shared__ uint64_t s_O[kRing];                 // tokens before the tile
+    __shared__ uint32_t s_C[kRing];                 // carry into the tile
+    __shared__ uint32_t s_ticket[kRing];
+    __shared__ uint32_t s_p1cnt[kRing];             // phase-1 arrivals per slot (kWaves per use); waves
+                                                    // drift across iterations, so one counter would mix them
+    __shared__ uint32_t s_rdone;                    // iterations whose tile is resolved
+    __shared__ uint32_t s_lbdone;                   // iterations whose pending tile has C, O
+    __shared__ uint32_t s_tkdone;                   // iterations whose next ticket is in s_ticket
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1043,8 +1086,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
     if (tid == 0) {
-        s_wfn[0][0] = atomicAdd(p.ctl, 1u);
-        s_wfn[0][1] = atomicAdd(p.ctl, 1u);
+        s_ticket[0] = atomicAdd(p.ctl, 1u);
+        s_ticket[1] = atomicAdd(p.ctl, 1u);
+        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
+        s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
@@ -1053,8 +1098,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
-    uint32_t T = uni(s_wfn[0][0]);    // tile in phase 1
-    uint32_t Tn = uni(s_wfn[0][1]);   // tile whose bytes are loaded during this iteration's emission
+    uint32_t T = uni(s_ticket[0]);    // tile in phase 1
+    uint32_t Tn = uni(s_ticket[1]);   // tile whose bytes are loaded during this iteration's emission
     uint32_t Tp = kNone;              // tile waiting for emission
     __syncthreads();
 
@@ -1064,42 +1109,64 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     TInfo ti = {}, tip = {};
     if (T < ntiles) ti = tile_info(p, T);
     TileState sp, sc;       // phase-1 state of Tp (pending) and of T (current)
-    uint32_t slot = 0;      // s_gin / s_tfn slot of T (Tp has slot ^ 1)
+    uint64_t lbs[kLbWin];   // wave 0: status words for the pending tile's look-back
 
-    while (T < ntiles || Tp < ntiles) {
+    for (uint32_t it = 0; T < ntiles || Tp < ntiles; ++it) {
+        const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
+        uint64_t stamp[7];
+        const bool stamping = p.debug != nullptr;
+        if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
-        const uint64_t ts0 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
+        if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
         // look-back loads for Tp fly during phase 1 (wave 0); ticket for the tile after Tn
-        uint64_t lbs[kLbWin];
         const bool lb = wave == 0 && Tp < ntiles && Tp > 0;
         if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
         uint32_t tk = kNone;
         if (tid == 64 && Tn < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
-        // ---- phase 1 of T ---------------------------------------------------------------------
-        if (T < ntiles) phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn);
+        // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
+        if (T < ntiles) {
+#if defined(BLT_EXP) && (BLT_EXP & 16)
+            if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
+#endif
+            phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
+            uint32_t old = 0;
+            if (lane == 0)
+                old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = uni(old);
+            if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
+                resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                if (lane == 0) lds_release(&s_rdone, it + 1u);
+            }
+        }
+        if (tid == 64) {
+            s_ticket[slot] = tk;
+            lds_release(&s_tkdone, it + 1u);
+        }
+        if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
         // ---- carry-in and offset of Tp (wave 0) --------------------------------------------
-        uint32_t spins = 0;
         if (wave == 0 && Tp < ntiles) {
-            uint32_t C = 1u, how = 0xFFFFu;
+            uint32_t C = 1u, how = 0xFFFFu, spins = 0;
             uint64_t O = 0ull;
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+            wait_ge(p, &s_rdone, it);   // Tp (resolved last iteration) has its tile function
             if (lane == 0) {
-                const uint32_t* tf = s_tfn[slot ^ 1u];
+                const uint32_t* tf = s_tfn[pslot];
                 const uint64_t end = O + (C ? tf[3] : tf[2]);
                 if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
                     record_error(p, 4u, Tp, 0xFFu, O, end, C);
                     O = 0; C = 1;
                 }
-                if (2ull * (O + (C ? tf[3] : tf[2])) > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, end, C);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf[1] : tf[0], O + (C ? tf[3] : tf[2])));
-                s_C = C;
-                s_O = O;
+                const uint64_t fin = O + (C ? tf[3] : tf[2]);
+                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf[1] : tf[0], fin));
+                s_C[pslot] = C;
+                s_O[pslot] = O;
                 if (Tp == ntiles - 1) {
-                    *p.total = O + (C ? tf[3] : tf[2]);
-                    if (p.chunk_off) p.chunk_off[p.nchunks] = O + (C ? tf[3] : tf[2]);
+                    *p.total = fin;
+                    if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
                 }
                 if (p.debug) {
                     uint64_t* d = p.debug + 4ull * Tp;
@@ -1107,40 +1174,48 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     d[1] = ((uint64_t)C << 32) | how;
                     d[2] = ((uint64_t)tf[3] << 32) | tf[2];
                     d[3] = ((uint64_t)tf[1] << 32) | tf[0];
+                    uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
+                    e[3] = spins;
                 }
+                lds_release(&s_lbdone, it + 1u);
             }
         }
-        if (tid == 64) s_ticket = tk;
-        const uint64_t tw0 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
-        __syncthreads();
-        const uint64_t ts1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
 
-        // ---- resolve and publish T (last wave) ----------------------------------------------
-        if (wave == kWaves - 1 && T < ntiles) resolve_tile(p, T, lane, s_wfn, s_gin[slot], s_tfn[slot]);
-
-        // ---- emit Tp; load Tn's bytes -------------------------------------------------------
-        if (Tp < ntiles) emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[slot ^ 1u], uni(s_C), uni64(s_O),
-                                   s_stage[wave]);
+        // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
+        // T's bytes are consumed: the loads fly during the emission
         if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
-        const uint64_t tw1 = p.debug ? __builtin_amdgcn_s_memtime() : 0;
-        __syncthreads();   // s_ticket, s_gin/s_tfn[slot], s_C/s_O, s_wfn reuse
-        if (p.debug && T < ntiles && lane == 0) {
-            // per wave: phase-1 work, first-barrier wait, emission work, second-barrier wait
-            const uint64_t tw2 = __builtin_amdgcn_s_memtime();
-            uint64_t* w = p.debug + 8ull * ntiles + 4ull * ((uint64_t)T * kWaves + wave);
-            w[0] = tw0 - ts0; w[1] = ts1 - tw0; w[2] = tw1 - ts1; w[3] = tw2 - tw1;
+        if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
+        if (Tp < ntiles) {
+            wait_ge(p, &s_lbdone, it + 1u);
+            if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
+#if defined(BLT_EXP) && (BLT_EXP & 8)
+            if (Tp == kNone - 1u)   // timing experiment: no emission
+#endif
+            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], uni(s_C[pslot]), uni64(s_O[pslot]),
+                      s_stage[wave]);
+        }
+        if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
+        uint32_t Tnn = kNone;
+        if (Tn < ntiles) {
+            wait_ge(p, &s_tkdone, it + 1u);
+            Tnn = uni(s_ticket[slot]);
+        }
+        if (stamping && Tp < ntiles && lane == 0) {
+            stamp[6] = __builtin_amdgcn_s_memtime();
+            uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
         }
         if (p.debug && tid == 0 && Tp < ntiles) {
-            uint64_t* d = p.debug + 4ull * ntiles + 4ull * Tp;
-            d[0] = ts0; d[1] = ts1; d[2] = __builtin_amdgcn_s_memtime(); d[3] = spins;
+            uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
+            e[2] = __builtin_amdgcn_s_memtime();
         }
         sp = sc;
         tip = ti;
         if (Tn < ntiles) ti = tile_info(p, Tn);
         Tp = T;
         T = Tn;
-        Tn = uni(s_ticket);
-        slot ^= 1u;
+        Tn = Tnn;
     }
 }
 

@@ -29,7 +29,7 @@ def main():
     wsb = s.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     ntiles = (n + TILE - 1) // TILE
-    dbg = torch.zeros((8 + 4 * 16) * ntiles, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros((8 + 8 * 16) * ntiles, dtype=torch.int64, device="cuda")
     L = blt_amd._lib.lib()
     L.blt_debug_set_tile_record.argtypes = [ctypes.c_void_p]
     sp = torch.cuda.current_stream().cuda_stream
@@ -39,20 +39,16 @@ def main():
     L.blt_debug_set_tile_record(None)
     rec = dbg.cpu().numpy().astype(np.int64)
     how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
-    st = rec[4 * ntiles:8 * ntiles].reshape(ntiles, 4)
-    ok = st[:, 0] != 0
-    p1, p2 = st[ok, 1] - st[ok, 0], st[ok, 2] - st[ok, 1]
-    for name, v in (("phase1+lookback", p1), ("resolve+emit", p2), ("iteration", p1 + p2)):
-        print(f"{name:16s} mean {v.mean():9.0f}  median {np.median(v):9.0f}  p90 {np.percentile(v, 90):9.0f} cycles")
-    sp = st[ok, 3]
-    print(f"look-back spins mean {sp.mean():.2f} median {np.median(sp)} p90 {np.percentile(sp, 90)} max {sp.max()}")
-    wv = rec[8 * ntiles:].reshape(ntiles, -1, 4)
-    okw = wv[:, 0, 0] > 0
-    wv = wv[okw]
-    print("per wave (mean cycles): phase1-work  B1-wait  emit-work  B2-wait")
-    for w in range(wv.shape[1]):
-        a = wv[:, w, :].mean(axis=0)
-        print(f"  wave {w:2d}: {a[0]:8.0f} {a[1]:8.0f} {a[2]:8.0f} {a[3]:8.0f}")
+    wv = rec[8 * ntiles:].reshape(ntiles, 16, 8)[:, :, :6]
+    ok = wv[:, 0, :].sum(axis=1) > 0
+    wv = wv[ok]
+    names = ["x-wait", "phase1", "lb+pub", "lb-wait", "emit", "tk-wait"]
+    print("per wave mean cycles: " + " ".join(f"{x:>8s}" for x in names) + "     total")
+    for w in range(16):
+        m = wv[:, w, :].mean(axis=0)
+        print(f"  wave {w:2d}:          " + " ".join(f"{v:8.0f}" for v in m) + f"  {m.sum():8.0f}")
+    sp = rec[4 * ntiles + 3:8 * ntiles:4]
+    print(f"look-back spins mean {sp.mean():.2f} max {sp.max()}")
     valid = how != 0xFFFF
     f, qs, rounds = how & 63, (how >> 6) & 3, how >> 8
     print("look-back: first-inclusive lane mean %.1f, window mean %.2f, extra rounds mean %.3f max %d" %
