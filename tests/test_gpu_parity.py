@@ -229,3 +229,16 @@ def test_columnar_tails(n):
     data = rng.integers(0, 3, n, dtype=np.uint8).tobytes()
     m = {(0, 1): 256, (1, 1): 257, (2, 0): 258, (1, 2): 259}
     assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+
+
+def test_many_tiles_per_workgroup():
+    """More tiles than 2 x workgroups (each workgroup claims tiles again and again) at two chunk
+    sizes, against the C oracle: 48 MiB = 1536 tiles of 32 KiB."""
+    text = synth.text(48 << 20, seed=5)
+    m = synth.merges_dict(synth.text_merges_50k(synth.text(8 << 20, seed=3), seed=3))
+    s = blt_amd.BpeStrategy(m)
+    for cs in (16 << 20, 1000003):
+        got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(m).run(text, cs, threads=16, return_lens=True)
+        assert np.array_equal(lens, elens)
+        assert np.array_equal(got, exp)
