@@ -60,7 +60,7 @@ def main():
     import torch.distributed as dist
 
     import blt_amd
-    from blt_amd import synth
+    from blt_amd import shard, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,7 +73,8 @@ def main():
     n = args.bytes_per_gpu
     merges = build_merges(synth)
     strategy = blt_amd.BpeStrategy(merges)
-    host = synth.text(n, seed=3, offset=rank * n)           # this rank's shard of the stream
+    b0, b1 = shard.rank_bytes(world * n, CHUNK, rank, world)   # this rank's chunk range of the stream
+    host = synth.text(b1 - b0, seed=3, offset=b0)
     d_in = torch.from_numpy(host).to("cuda")
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     nchunks = (n + CHUNK - 1) // CHUNK
@@ -112,10 +113,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tokens = int(d_off[-1].item())
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = float(t[0]), float(t[1])
+    elapsed, kern_ms_max = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
 

@@ -10,6 +10,8 @@ Python mirror of the reference's strategy surface over the C ABI in include/blt_
   (utils.rs:10-45, chunking.rs:26-62, utils.rs:79-97)
 * ``BpeStrategy.process_chunks(data, chunk_size, n_gpus)``  — the mmap pipeline's chunk split and
   ordered stitch (pipeline.rs:56-192), sharded over GPUs.
+* ``PassthroughStrategy``, ``select_strategy``, ``run_tokenizer`` — strategy choice
+  (lib.rs:271-282), content-type token (lib.rs:284-293) and the chunked pipeline over a buffer.
 
 All tokenising calls run the HIP kernels in libblt_bpe.so; there is no CPU fallback.
 """
@@ -22,7 +24,8 @@ from . import _lib
 from ._lib import BltError
 
 __all__ = [
-    "BltError", "TokenizationStrategy", "BpeStrategy", "BasicTokenizationStrategy", "ContentType",
+    "BltError", "TokenizationStrategy", "BpeStrategy", "BasicTokenizationStrategy", "PassthroughStrategy",
+    "ContentType", "select_strategy", "run_tokenizer",
     "load_bpe_merges_from_path", "load_bpe_merges", "parse_chunk_size_str", "get_effective_chunk_size",
     "determine_thread_count", "version",
 ]
@@ -220,3 +223,35 @@ class BasicTokenizationStrategy(TokenizationStrategy):
 
     def encode_device(self, d_in: int, n: int, d_out: int, stream: int = 0) -> None:
         _lib.check(self._L.blt_basic_encode_device(d_in, n, d_out, stream or None))
+
+
+class PassthroughStrategy(TokenizationStrategy):
+    """PassthroughStrategy (tokenizer.rs:126-145): returns the chunk unchanged (copy mode)."""
+
+    def process_chunk(self, chunk_data) -> bytes:
+        return bytes(memoryview(chunk_data).cast("B"))
+
+
+def select_strategy(bpe_merges: Optional[Dict[Tuple[int, int], int]] = None, passthrough: bool = False):
+    """select_strategy (lib.rs:271-282): passthrough > BPE (if merges) > basic."""
+    if passthrough:
+        return PassthroughStrategy()
+    if bpe_merges is not None:
+        return BpeStrategy.new(bpe_merges)
+    return BasicTokenizationStrategy()
+
+
+def run_tokenizer(data, chunk_size: int, strategy: TokenizationStrategy, content_type: Optional[str] = None,
+                  n_gpus: int = 1) -> bytes:
+    """run_tokenizer over an in-memory buffer (lib.rs:239-265): the optional content-type token
+    (lib.rs:284-293), then every chunk of chunk_size bytes (pipeline.rs:73-81) tokenised and
+    stitched in chunk order (pipeline.rs:153-192).  BPE runs as one batched GPU call."""
+    head = b"" if content_type is None else ContentType.BY_NAME[content_type].to_bytes(2, "big")
+    if chunk_size <= 0:
+        raise ValueError("chunk_size must be > 0")
+    if isinstance(strategy, BpeStrategy):
+        import numpy as np
+        return head + bytes(np.asarray(strategy.process_chunks(data, chunk_size, n_gpus=n_gpus)))
+    mv = memoryview(data).cast("B")
+    # basic and passthrough are per byte: the chunk split does not change the stream
+    return head + strategy.process_chunk(mv) if len(mv) else head
