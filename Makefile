@@ -11,9 +11,10 @@ CC ?= gcc
 LIB := blt_amd/libblt_bpe.so
 SYNTH := blt_amd/libblt_synth.so
 ORACLE := oracle/liboracle.so
+CLI := blt_amd/blt
 OBJDIR := build
 
-all: $(LIB) $(SYNTH) $(ORACLE)
+all: $(LIB) $(SYNTH) $(ORACLE) $(CLI)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -27,6 +28,10 @@ $(OBJDIR)/blt_host.o: blt_amd/csrc/blt_host.cpp blt_amd/csrc/bpe_kernels.h inclu
 $(LIB): $(OBJDIR)/bpe_kernels.o $(OBJDIR)/blt_host.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -lpthread
 
+# the `blt` command line (src/main.rs drop-in), linked against the library next to it
+$(CLI): blt_amd/csrc/blt_cli.cpp include/blt_bpe.h $(LIB)
+	$(CXX) -O2 -std=c++17 -Wall -pthread -o $@ $< -Lblt_amd -lblt_bpe -Wl,-rpath,'$$ORIGIN'
+
 $(SYNTH): blt_amd/csrc/synth.c
 	$(CC) -O2 -fPIC -fopenmp -shared -o $@ $<
 
@@ -34,13 +39,13 @@ $(ORACLE): oracle/bpe_oracle.c
 	$(MAKE) -C oracle liboracle.so
 
 clean:
-	rm -rf $(OBJDIR) $(LIB) $(SYNTH) $(ORACLE)
+	rm -rf $(OBJDIR) $(LIB) $(SYNTH) $(ORACLE) $(CLI)
 
 .PHONY: all clean
 
 # Timing experiments (tools/tile_timing.py with BLT_LIB_PATH): kernel variants with parts of
 # the work removed.  Wrong output by construction; never used by the product or the tests.
-EXPS := 1 2 4 6 7 8 16 24
+EXPS := 1 2 4 256
 exp: $(foreach e,$(EXPS),build/exp/libblt_bpe_exp$(e).so)
 build/exp/libblt_bpe_exp%.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
 	mkdir -p build/exp

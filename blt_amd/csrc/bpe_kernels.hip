@@ -837,7 +837,7 @@ struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never 
 };
 
 __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (&s)[kLbWin], uint32_t& C,
-                          uint64_t& O, uint32_t& how, uint32_t& spins) {
+                          uint64_t& O, uint32_t& how, uint32_t& spins, uint32_t* bad_out = nullptr) {
     TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
     int64_t k = (int64_t)Tp - 1;
     uint32_t rounds = 0;
@@ -858,6 +858,15 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                     ready = false;
                 }
             }
+        }
+        if (!ready && spins == 0 && bad_out) {   // debug: distance of the first tile not ready
+            uint32_t d = 0;
+#pragma unroll
+            for (int q = kLbWin - 1; q >= 0; --q) {
+                const uint64_t rdy = __ballot((uint32_t)(s[q] >> 62) != 0u);
+                if (rdy != ~0ull) d = 64u * (uint32_t)q + (uint32_t)__builtin_ctzll(~rdy) + 1u;
+            }
+            *bad_out = d;
         }
         if (!ready) {
             if (++spins > kLbSpinLimit) {
@@ -1086,8 +1095,13 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
     if (tid == 0) {
+#if defined(BLT_EXP) && (BLT_EXP & 256)
+        s_ticket[0] = blockIdx.x;                 // timing experiment: static round-robin tiles
+        s_ticket[1] = blockIdx.x + gridDim.x;
+#else
         s_ticket[0] = atomicAdd(p.ctl, 1u);
         s_ticket[1] = atomicAdd(p.ctl, 1u);
+#endif
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
@@ -1121,8 +1135,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // look-back loads for Tp fly during phase 1 (wave 0); ticket for the tile after Tn
         const bool lb = wave == 0 && Tp < ntiles && Tp > 0;
         if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+        uint64_t rt_snap = 0;
+        if (p.debug && lb) rt_snap = __builtin_amdgcn_s_memrealtime();
         uint32_t tk = kNone;
+#if defined(BLT_EXP) && (BLT_EXP & 256)
+        if (tid == 64 && Tn < ntiles) tk = Tn + gridDim.x;
+#else
         if (tid == 64 && Tn < ntiles) tk = atomicAdd(p.ctl, 1u);
+#endif
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
@@ -1138,6 +1158,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
+                if (p.debug && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
         if (tid == 64) {
@@ -1148,9 +1169,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 
         // ---- carry-in and offset of Tp (wave 0) --------------------------------------------
         if (wave == 0 && Tp < ntiles) {
-            uint32_t C = 1u, how = 0xFFFFu, spins = 0;
+            uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, &bad);
             wait_ge(p, &s_rdone, it);   // Tp (resolved last iteration) has its tile function
             if (lane == 0) {
                 const uint32_t* tf = s_tfn[pslot];
@@ -1175,7 +1196,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     d[2] = ((uint64_t)tf[3] << 32) | tf[2];
                     d[3] = ((uint64_t)tf[1] << 32) | tf[0];
                     uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
-                    e[3] = spins;
+                    e[3] = spins | ((uint64_t)bad << 32);
+                    e[1] = (rt_snap & 0xFFFFFFFFull) | (__builtin_amdgcn_s_memrealtime() << 32);
                 }
                 lds_release(&s_lbdone, it + 1u);
             }

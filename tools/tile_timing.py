@@ -47,8 +47,45 @@ def main():
     for w in range(16):
         m = wv[:, w, :].mean(axis=0)
         print(f"  wave {w:2d}:          " + " ".join(f"{v:8.0f}" for v in m) + f"  {m.sum():8.0f}")
-    sp = rec[4 * ntiles + 3:8 * ntiles:4]
+    sp = rec[4 * ntiles + 3:8 * ntiles:4] & 0xFFFFFFFF
+    bad = rec[4 * ntiles + 3:8 * ntiles:4] >> 32
     print(f"look-back spins mean {sp.mean():.2f} max {sp.max()}")
+    # s_memrealtime (100 MHz, one clock for the whole chip): aggregate publish of each tile,
+    # look-back snapshot issue and completion of its successor's look-back
+    pub = rec[4 * ntiles:8 * ntiles:4]
+    snap = rec[4 * ntiles + 1:8 * ntiles:4] & 0xFFFFFFFF
+    done = (rec[4 * ntiles + 1:8 * ntiles:4] >> 32) & 0xFFFFFFFF
+    pub32 = pub & 0xFFFFFFFF
+    t = np.arange(2, ntiles)
+    gap = ((snap[t] - pub32[t - 1] + (1 << 31)) % (1 << 32)) - (1 << 31)   # snapshot - predecessor publish
+    wait = ((done[t] - snap[t] + (1 << 31)) % (1 << 32)) - (1 << 31)
+    spt = sp[t]
+    us = lambda v: v / 100.0
+    for k in range(0, 4):
+        sel = spt == k if k < 3 else spt >= 3
+        if sel.any():
+            print(f"spins {k}{'+' if k == 3 else ' '}: {sel.sum():6d} tiles; snapshot - pred publish us "
+                  f"p10 {us(np.percentile(gap[sel], 10)):6.2f} p50 {us(np.median(gap[sel])):6.2f} "
+                  f"p90 {us(np.percentile(gap[sel], 90)):6.2f}; look-back us p50 {us(np.median(wait[sel])):6.2f}")
+    hist = np.histogram(us(gap), bins=[-100, -4, -2, -1, 0, 1, 2, 3, 4, 6, 8, 100])
+    print("gap histogram (us):", list(zip(hist[1][:-1].tolist(), hist[0].tolist())))
+    # spin probability as a function of the gap
+    for lo, hi in [(-100, 0), (0, 1), (1, 2), (2, 3), (3, 4), (4, 6), (6, 100)]:
+        sel = (us(gap) >= lo) & (us(gap) < hi)
+        if sel.any():
+            print(f"  gap [{lo},{hi}) us: n {sel.sum():6d}, P(spin) {(spt[sel] > 0).mean():.2f}")
+    # the first tile found not ready: its distance back, and its publish time vs the snapshot
+    sel = np.nonzero(bad[t] > 0)[0]
+    if sel.size:
+        tt = t[sel]
+        d = bad[tt]
+        print("first not-ready tile distance: p10 %d p50 %d p90 %d max %d; share at distance 1: %.2f" %
+              (np.percentile(d, 10), np.median(d), np.percentile(d, 90), d.max(), (d == 1).mean()))
+        src = tt - d
+        okk = src >= 0
+        g2 = ((snap[tt[okk]] - pub32[src[okk]] + (1 << 31)) % (1 << 32)) - (1 << 31)
+        print("  its publish vs snapshot (snapshot - publish) us: p10 %.2f p50 %.2f p90 %.2f" %
+              (us(np.percentile(g2, 10)), us(np.median(g2)), us(np.percentile(g2, 90))))
     valid = how != 0xFFFF
     f, qs, rounds = how & 63, (how >> 6) & 3, how >> 8
     print("look-back: first-inclusive lane mean %.1f, window mean %.2f, extra rounds mean %.3f max %d" %
