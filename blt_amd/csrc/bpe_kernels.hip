@@ -1097,10 +1097,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     if (tid == 0) {
 #if defined(BLT_EXP) && (BLT_EXP & 256)
         s_ticket[0] = blockIdx.x;                 // timing experiment: static round-robin tiles
-        s_ticket[1] = blockIdx.x + gridDim.x;
 #else
         s_ticket[0] = atomicAdd(p.ctl, 1u);
-        s_ticket[1] = atomicAdd(p.ctl, 1u);
 #endif
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
@@ -1113,7 +1111,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
     uint32_t T = uni(s_ticket[0]);    // tile in phase 1
-    uint32_t Tn = uni(s_ticket[1]);   // tile whose bytes are loaded during this iteration's emission
     uint32_t Tp = kNone;              // tile waiting for emission
     __syncthreads();
 
@@ -1137,11 +1134,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
         uint64_t rt_snap = 0;
         if (p.debug && lb) rt_snap = __builtin_amdgcn_s_memrealtime();
+        // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
+        // bytes are needed, so claim order stays close to publish order (a tile claimed two
+        // iterations ahead lands behind later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (tid == 64 && Tn < ntiles) tk = Tn + gridDim.x;
+        if (tid == 64 && T < ntiles) tk = T + gridDim.x;
 #else
-        if (tid == 64 && Tn < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (tid == 64 && T < ntiles) tk = atomicAdd(p.ctl, 1u);
 #endif
         asm volatile("" ::: "memory");
 
@@ -1205,6 +1205,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
         // T's bytes are consumed: the loads fly during the emission
+        uint32_t Tn = kNone;
+        if (T < ntiles) {
+            wait_ge(p, &s_tkdone, it + 1u);
+            Tn = uni(s_ticket[slot]);
+            if (Tn >= ntiles) Tn = kNone;
+        }
         if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
         if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
@@ -1217,11 +1223,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                       s_stage[wave]);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
-        uint32_t Tnn = kNone;
-        if (Tn < ntiles) {
-            wait_ge(p, &s_tkdone, it + 1u);
-            Tnn = uni(s_ticket[slot]);
-        }
         if (stamping && Tp < ntiles && lane == 0) {
             stamp[6] = __builtin_amdgcn_s_memtime();
             uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
@@ -1237,7 +1238,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (Tn < ntiles) ti = tile_info(p, Tn);
         Tp = T;
         T = Tn;
-        Tn = Tnn;
     }
 }
 
