@@ -45,7 +45,7 @@ clean:
 
 # Timing experiments (tools/tile_timing.py with BLT_LIB_PATH): kernel variants with parts of
 # the work removed.  Wrong output by construction; never used by the product or the tests.
-EXPS := 1 2 4 256 1024
+EXPS := 1 2 4 256 2048
 exp: $(foreach e,$(EXPS),build/exp/libblt_bpe_exp$(e).so)
 build/exp/libblt_bpe_exp%.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
 	mkdir -p build/exp

@@ -1171,20 +1171,24 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (wave == 0 && Tp < ntiles) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
+            // Tp was resolved last iteration: its tile function is read while the snapshot flies
+            wait_ge(p, &s_rdone, it);
+            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, &bad);
-            wait_ge(p, &s_rdone, it);   // Tp (resolved last iteration) has its tile function
             if (lane == 0) {
-                const uint32_t* tf = s_tfn[pslot];
-                const uint64_t end = O + (C ? tf[3] : tf[2]);
+                const uint64_t end = O + (C ? tf3 : tf2);
                 if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
                     record_error(p, 4u, Tp, 0xFFu, O, end, C);
                     O = 0; C = 1;
                 }
-                const uint64_t fin = O + (C ? tf[3] : tf[2]);
-                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf[1] : tf[0], fin));
+                // the other waves need only C and O: release them first, publish after
                 s_C[pslot] = C;
                 s_O[pslot] = O;
+                lds_release(&s_lbdone, it + 1u);
+                const uint64_t fin = O + (C ? tf3 : tf2);
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
+                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
                     *p.total = fin;
                     if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
@@ -1193,13 +1197,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     uint64_t* d = p.debug + 4ull * Tp;
                     d[0] = O;
                     d[1] = ((uint64_t)C << 32) | how;
-                    d[2] = ((uint64_t)tf[3] << 32) | tf[2];
-                    d[3] = ((uint64_t)tf[1] << 32) | tf[0];
+                    d[2] = ((uint64_t)tf3 << 32) | tf2;
+                    d[3] = ((uint64_t)tf1 << 32) | tf0;
                     uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
                     e[3] = spins | ((uint64_t)bad << 32);
                     e[1] = (rt_snap & 0xFFFFFFFFull) | (__builtin_amdgcn_s_memrealtime() << 32);
                 }
-                lds_release(&s_lbdone, it + 1u);
             }
         }
 
