@@ -1052,6 +1052,15 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 // (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
 constexpr int kRing = 4;
 constexpr uint32_t kWaitLimit = 1u << 22;
+// Wave priorities (s_setprio) during phase 1 and emission: waves >= k*Wave get k*.  BLT_PRIO
+// (timing sweeps only) = P1 wave * 1e6 + P1 priority * 1e4 + emission wave * 100 + priority.
+#ifdef BLT_PRIO
+constexpr int kPrioP1Wave = BLT_PRIO / 1000000, kPrioP1 = (BLT_PRIO / 10000) % 100;
+constexpr int kPrioEmWave = (BLT_PRIO / 100) % 100, kPrioEm = BLT_PRIO % 100;
+#else
+constexpr int kPrioP1Wave = 8, kPrioP1 = 1;
+constexpr int kPrioEmWave = 12, kPrioEm = 2;
+#endif
 
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
     return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1150,7 +1159,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #if defined(BLT_EXP) && (BLT_EXP & 16)
             if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
 #endif
+            // issue priority by age: the youngest waves lose the arbiter to the older ones, finish
+            // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
+            // look-backs wait for), and finish emission last (which holds back their next phase 1)
+            if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
             phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
+            __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1222,8 +1236,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #if defined(BLT_EXP) && (BLT_EXP & 8)
             if (Tp == kNone - 1u)   // timing experiment: no emission
 #endif
+            if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
             emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], uni(s_C[pslot]), uni64(s_O[pslot]),
                       s_stage[wave]);
+            __builtin_amdgcn_s_setprio(0);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
         if (stamping && Tp < ntiles && lane == 0) {
