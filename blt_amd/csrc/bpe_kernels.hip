@@ -1052,6 +1052,13 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 // (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
 constexpr int kRing = 4;
 constexpr uint32_t kWaitLimit = 1u << 22;
+// Per-wave phase stamps and look-back timing (tools/tile_timing.py) only in the timing build
+// (-DBLT_TIMING): kept live across the loop they cost scalar registers the kernel has none of.
+#ifdef BLT_TIMING
+constexpr bool kTiming = true;
+#else
+constexpr bool kTiming = false;
+#endif
 // Wave priorities (s_setprio) during phase 1 and emission: waves >= k*Wave get k*.  BLT_PRIO
 // (timing sweeps only) = P1 wave * 1e6 + P1 priority * 1e4 + emission wave * 100 + priority.
 #ifdef BLT_PRIO
@@ -1134,7 +1141,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     for (uint32_t it = 0; T < ntiles || Tp < ntiles; ++it) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
         uint64_t stamp[7];
-        const bool stamping = p.debug != nullptr;
+        const bool stamping = kTiming && p.debug != nullptr;
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
@@ -1142,7 +1149,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         const bool lb = wave == 0 && Tp < ntiles && Tp > 0;
         if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
         uint64_t rt_snap = 0;
-        if (p.debug && lb) rt_snap = __builtin_amdgcn_s_memrealtime();
+        if (stamping && lb) rt_snap = __builtin_amdgcn_s_memrealtime();
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
@@ -1172,7 +1179,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
-                if (p.debug && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
+                if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
         if (tid == 64) {
@@ -1189,7 +1196,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             wait_ge(p, &s_rdone, it);
             const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
             const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, &bad);
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, kTiming ? &bad : nullptr);
             if (lane == 0) {
                 const uint64_t end = O + (C ? tf3 : tf2);
                 if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
@@ -1213,9 +1220,11 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     d[1] = ((uint64_t)C << 32) | how;
                     d[2] = ((uint64_t)tf3 << 32) | tf2;
                     d[3] = ((uint64_t)tf1 << 32) | tf0;
-                    uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
-                    e[3] = spins | ((uint64_t)bad << 32);
-                    e[1] = (rt_snap & 0xFFFFFFFFull) | (__builtin_amdgcn_s_memrealtime() << 32);
+                    if (kTiming) {
+                        uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
+                        e[3] = spins | ((uint64_t)bad << 32);
+                        e[1] = (rt_snap & 0xFFFFFFFFull) | (__builtin_amdgcn_s_memrealtime() << 32);
+                    }
                 }
             }
         }
@@ -1248,7 +1257,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
         }
-        if (p.debug && tid == 0 && Tp < ntiles) {
+        if (stamping && tid == 0 && Tp < ntiles) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
             e[2] = __builtin_amdgcn_s_memtime();
         }

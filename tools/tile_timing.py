@@ -1,4 +1,5 @@
-"""Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook).
+"""Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook, in
+the timing build build/exp/libblt_bpe_timing.so from `make exp`, or BLT_LIB_PATH).
 
     python tools/tile_timing.py [MiB]
 Prints mean/median cycles of phase 1 (lookups + wave functions), phase 2 (tile resolve +
@@ -9,7 +10,10 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+# the stamps exist only in the timing build of the kernel (make exp; -DBLT_TIMING)
+os.environ.setdefault("BLT_LIB_PATH", os.path.join(ROOT, "build", "exp", "libblt_bpe_timing.so"))
 import torch  # noqa: E402
 
 import blt_amd  # noqa: E402
