@@ -917,6 +917,53 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
     }
 }
 
+// ---- dense wave ranges ----------------------------------------------------------------------
+// Every pair of a wave range merges (text under a large merge map): every lane is an identity
+// function, so all lanes take the wave's carry-in c and emit exactly 8 tokens - the low halves
+// of v (c = 1, positions 0, 2, .., 14) or the high halves (c = 0, positions 1, 3, .., 15).  A lane
+// packs them into 16 bytes; the stage places token n of the range at byte rg + 2n, so the aligned
+// 16-byte block l holds the last rg/2 tokens of lane l-1 and the first 8 - rg/2 of lane l: one
+// DPP fetch, a funnel shift and one conflict-free ds_write_b128 per lane (lane 63 also writes the
+// block after the range).  Bytes of block 0 before rg are garbage the copy-out never reads.
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
+    return r ? __builtin_amdgcn_alignbyte(hi, lo, 2) : lo;   // r in {0, 2}
+}
+__device__ __forceinline__ u32x4 block_of(const u32x4& a, const u32x4& b, uint32_t d, uint32_t r) {
+    // bytes [4d + r, 4d + r + 16) of the 32-byte concatenation a ++ b (d in 0..3, uniform)
+    u32x4 o;
+    if (d == 0) {
+        o[0] = funnel(a[1], a[0], r); o[1] = funnel(a[2], a[1], r); o[2] = funnel(a[3], a[2], r); o[3] = funnel(b[0], a[3], r);
+    } else if (d == 1) {
+        o[0] = funnel(a[2], a[1], r); o[1] = funnel(a[3], a[2], r); o[2] = funnel(b[0], a[3], r); o[3] = funnel(b[1], b[0], r);
+    } else if (d == 2) {
+        o[0] = funnel(a[3], a[2], r); o[1] = funnel(b[0], a[3], r); o[2] = funnel(b[1], b[0], r); o[3] = funnel(b[2], b[1], r);
+    } else {
+        o[0] = funnel(b[0], a[3], r); o[1] = funnel(b[1], b[0], r); o[2] = funnel(b[2], b[1], r); o[3] = funnel(b[3], b[2], r);
+    }
+    return o;
+}
+__device__ __forceinline__ void stage_dense(const uint32_t (&v)[8], uint32_t c, uint32_t rg, uint32_t stg_lds, int lane) {
+    const uint32_t sel = c ? 0x05040100u : 0x07060302u;   // low halves (c = 1) or high halves (c = 0)
+    u32x4 P;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
+    if (rg == 0) {
+        *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * (uint32_t)lane) = P;
+        return;
+    }
+    u32x4 Q;   // lane l - 1's tokens (lane 0: garbage, lands before rg)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
+    const uint32_t off = 16u - rg;   // block l = bytes [16 - rg, 32 - rg) of Q ++ P
+    const uint32_t d = off >> 2, r = off & 3u;
+    *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * (uint32_t)lane) = block_of(Q, P, d, r);
+    if (lane == 63) {   // block 64: lane 63's last rg / 2 tokens
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * 64u) = block_of(P, z, d, r);
+    }
+}
+
 // ---- emission of the pending tile --------------------------------------------------------
 // Tile-level: carry-in C, O tokens before the tile; the output resource starts at the 16-byte
 // boundary at or below byte 2 O, so every offset below is 32-bit.
@@ -967,6 +1014,9 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             continue;
         }
         uint32_t a = stg_lds + rg + 2u * lane_off;          // LDS byte address of this lane's next token
+        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {       // dense: every pair merges, no buffer end
+            stage_dense(st.v[j], cg, rg, stg_lds, lane);
+        } else
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             const uint32_t tok = st.v[j][h];

@@ -242,3 +242,18 @@ def test_many_tiles_per_workgroup():
         exp, elens = O.COracle(m).run(text, cs, threads=16, return_lens=True)
         assert np.array_equal(lens, elens)
         assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("cs", [4096, 4097, 6001, 65537, 1 << 20])
+def test_dense_wave_ranges(cs):
+    """Every pair merges (the byte pass's dense-range stage path): all 16-byte stage
+    alignments, carry-in 0 and 1 (odd chunk sizes shift the landing parity), chunk ends and the
+    buffer end falling back to the general path inside otherwise dense tiles."""
+    rng = np.random.default_rng(cs)
+    n = 4 * (1 << 20) + 777
+    data = rng.integers(97, 101, n, dtype=np.uint8)
+    m = {(a, b): 300 + 4 * (a - 97) + (b - 97) for a in range(97, 101) for b in range(97, 101)}
+    got, lens = blt_amd.BpeStrategy(m).process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
