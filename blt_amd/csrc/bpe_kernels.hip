@@ -1195,11 +1195,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-        // look-back loads for Tp fly during phase 1 (wave 0); ticket for the tile after Tn
-        const bool lb = wave == 0 && Tp < ntiles && Tp > 0;
-        if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
-        uint64_t rt_snap = 0;
-        if (stamping && lb) rt_snap = __builtin_amdgcn_s_memrealtime();
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
@@ -1212,6 +1207,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
+        bool lbw = wave == 0;   // the wave that resolves Tp: the first to finish phase 1
         if (T < ntiles) {
 #if defined(BLT_EXP) && (BLT_EXP & 16)
             if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
@@ -1226,6 +1222,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
+            lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
@@ -1238,10 +1235,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         }
         if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
-        // ---- carry-in and offset of Tp (wave 0) --------------------------------------------
-        if (wave == 0 && Tp < ntiles) {
+        // ---- carry-in and offset of Tp, by the first wave to finish phase 1: its snapshot is
+        // the freshest that still lands before the slower waves finish (~0.5 us round trip)
+        if (lbw && Tp < ntiles) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
+            const bool lb = Tp > 0;
+            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone, it);
             const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
