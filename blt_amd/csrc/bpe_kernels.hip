@@ -567,7 +567,7 @@ constexpr int kGroups = kS * kWaves;
 // 521 (2-byte aligned start + up to 1042 bytes) — every range of a text whose pairs mostly merge.
 // A range with more tokens stores them straight to global memory (emit_direct).
 constexpr int kStageWave = 1056;
-constexpr int kLbWin = 4;                              // look-back windows of 64 per round trip
+constexpr int kLbWin = 1;                              // look-back windows of 64 per round trip
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
