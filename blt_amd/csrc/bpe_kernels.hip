@@ -820,13 +820,25 @@ __device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lan
 // carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.
 __device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot) {
     const bool in = lane < lim;
-    const uint32_t co0 = (uint32_t)(s >> 60) & 1u, co1 = (uint32_t)(s >> 61) & 1u;
-    const bool ident = co0 == 0u && co1 == 1u;
+    const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
+    const uint32_t co0 = (hi >> 28) & 1u;
+    const bool ident = ((hi >> 28) & 3u) == 2u;   // co0 = 0, co1 = 1
+    const uint64_t inm = __ballot(in);
     const uint64_t nonid = __ballot(in && !ident);
     const uint64_t comask = __ballot(in && co0);   // a non-identity function is constant
-    const uint64_t older = nonid & ~((~0ull) >> (63 - lane));
-    const uint32_t cin = older ? (uint32_t)((comask >> __builtin_ctzll(older)) & 1ull) : c;
-    const uint32_t cnt = in ? (uint32_t)(cin ? (s >> 30) & 0x3FFFFFFFull : s & 0x3FFFFFFFull) : 0u;
+    uint32_t cin;
+    if (nonid == 0) {
+        cin = c;                                   // identities only (dense text): c runs through
+    } else if (nonid == inm) {
+        // constants only (ordinary text): a lane's carry-in is the next older lane's carry-out;
+        // the oldest lane in the window takes c
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)co0, (int)co0, 0x130, 0xF, 0xF, false);
+        cin = lane + 1 < lim ? up : c;
+    } else {
+        const uint64_t older = nonid & ~((~0ull) >> (63 - lane));
+        cin = older ? (uint32_t)((comask >> __builtin_ctzll(older)) & 1ull) : c;
+    }
+    const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x3FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
     tot += lane_u32(wave_scan(cnt), 63);
     return nonid ? (uint32_t)((comask >> __builtin_ctzll(nonid)) & 1ull) : c;
 }
