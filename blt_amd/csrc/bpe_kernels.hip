@@ -558,7 +558,9 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
 }
 
 constexpr int kThreads = 1024;                         // 16 waves: 4 per SIMD hide LDS and VALU latency
-constexpr int kWaves = kThreads / 64;
+constexpr int kTeams = BLT_TEAMS;                      // independent tile streams per workgroup
+constexpr int kAllWaves = kThreads / 64;
+constexpr int kWaves = kAllWaves / kTeams;             // waves per team: the tile geometry
 constexpr int kS = 2;                                  // sub-tiles per tile
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
@@ -1127,8 +1129,15 @@ constexpr bool kTiming = false;
 constexpr int kPrioP1Wave = BLT_PRIO / 1000000, kPrioP1 = (BLT_PRIO / 10000) % 100;
 constexpr int kPrioEmWave = (BLT_PRIO / 100) % 100, kPrioEm = BLT_PRIO % 100;
 #else
-constexpr int kPrioP1Wave = 8, kPrioP1 = 1;
-constexpr int kPrioEmWave = 12, kPrioEm = 2;
+constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
+constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
+#endif
+// Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
+// iteration (a whole iteration to land) and claims tickets two tiles ahead.
+#ifdef BLT_PF
+constexpr bool kPf = BLT_PF != 0;
+#else
+constexpr bool kPf = false;
 #endif
 
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
@@ -1152,34 +1161,43 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
 template <bool kBE>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
-    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroups][4];   // wave functions (phase 1)
-    __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
-    __shared__ uint32_t s_tfn[kRing][4];            // tile co0, co1, tot0, tot1
-    __shared__ uint64_t s_O[kRing];                 // tokens before the tile
-    __shared__ uint32_t s_C[kRing];                 // carry into the tile
-    __shared__ uint32_t s_ticket[kRing];
-    __shared__ uint32_t s_p1cnt[kRing];             // phase-1 arrivals per slot (kWaves per use); waves
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kAllWaves][kStageWave];
+    // per team:
+    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kTeams][kRing][kGroups][4];   // wave functions (phase 1)
+    __shared__ uint32_t s_gin[kTeams][kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
+    __shared__ uint32_t s_tfn[kTeams][kRing][4];            // tile co0, co1, tot0, tot1
+    __shared__ uint64_t s_O[kTeams][kRing];                 // tokens before the tile
+    __shared__ uint32_t s_C[kTeams][kRing];                 // carry into the tile
+    __shared__ uint32_t s_ticket[kTeams][kRing];
+    __shared__ uint32_t s_p1cnt[kTeams][kRing];     // phase-1 arrivals per slot (kWaves per use); waves
                                                     // drift across iterations, so one counter would mix them
-    __shared__ uint32_t s_rdone;                    // iterations whose tile is resolved
-    __shared__ uint32_t s_lbdone;                   // iterations whose pending tile has C, O
-    __shared__ uint32_t s_tkdone;                   // iterations whose next ticket is in s_ticket
+    __shared__ uint32_t s_rdone[kTeams];            // iterations whose tile is resolved
+    __shared__ uint32_t s_lbdone[kTeams];           // iterations whose pending tile has C, O
+    __shared__ uint32_t s_tkdone[kTeams];           // iterations whose next ticket is in s_ticket
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t wave = uni((uint32_t)tid >> 6);
+    const uint32_t gw = uni((uint32_t)tid >> 6);          // wave of the workgroup
+    const uint32_t team = kTeams == 1 ? 0u : gw / kWaves;          // team
+    const uint32_t wave = kTeams == 1 ? gw : gw % kWaves;          // wave within the team
+    const int ttid = kTeams == 1 ? tid : tid % (kWaves * 64);      // thread within the team
     const uint64_t n = p.n;
     const uint32_t ntiles = p.ntiles;
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
-    if (tid == 0) {
+    if (ttid == 0) {
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        s_ticket[0] = blockIdx.x;                 // timing experiment: static round-robin tiles
+        s_ticket[team][0] = blockIdx.x * kTeams + team;                 // timing experiment: static round-robin tiles
 #else
-        s_ticket[0] = atomicAdd(p.ctl, 1u);
+        s_ticket[team][0] = atomicAdd(p.ctl, 1u);
 #endif
-        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
-        s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
+#if defined(BLT_EXP) && (BLT_EXP & 256)
+        if (kPf) s_ticket[team][1] = s_ticket[team][0] + gridDim.x * kTeams;
+#else
+        if (kPf) s_ticket[team][1] = atomicAdd(p.ctl, 1u);   // the tile after it (prefetched in iteration 0)
+#endif
+        for (int r = 0; r < kRing; ++r) s_p1cnt[team][r] = 0;
+        s_rdone[team] = 0; s_lbdone[team] = 0; s_tkdone[team] = 0;
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
@@ -1188,12 +1206,16 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
-    uint32_t T = uni(s_ticket[0]);    // tile in phase 1
+    uint32_t T = uni(s_ticket[team][0]);    // tile in phase 1
     uint32_t Tp = kNone;              // tile waiting for emission
+    uint32_t Tq = kNone;              // kPf: the tile after T (its bytes are loaded during T's iteration)
+    if (kPf) { Tq = uni(s_ticket[team][1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
     __syncthreads();
 
     uint32_t x[kS][4];      // input bytes of each sub-tile of T
     uint32_t nxt[kS];       // byte after each wave range (lane 63's right neighbour)
+    uint32_t xq[kS][4];     // kPf: bytes of Tq
+    uint32_t nxtq[kS];
     if (T < ntiles) load_tile(p, T, wave, lane, x, nxt);
     TInfo ti = {}, tip = {};
     if (T < ntiles) ti = tile_info(p, T);
@@ -1207,14 +1229,15 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
+        if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (tid == 64 && T < ntiles) tk = T + gridDim.x;
+        if (ttid == 64 && (kPf ? Tq : T) < ntiles) tk = (kPf ? Tq : T) + gridDim.x * kTeams;
 #else
-        if (tid == 64 && T < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (ttid == 64 && (kPf ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
 #endif
         asm volatile("" ::: "memory");
 
@@ -1228,22 +1251,22 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
+            phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[team][slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
-                old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __hip_atomic_fetch_add(&s_p1cnt[team][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
             lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
-                if (lane == 0) lds_release(&s_rdone, it + 1u);
+                resolve_tile(p, T, lane, s_wfn[team][slot], s_gin[team][slot], s_tfn[team][slot]);
+                if (lane == 0) lds_release(&s_rdone[team], it + 1u);
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        if (tid == 64) {
-            s_ticket[slot] = tk;
-            lds_release(&s_tkdone, it + 1u);
+        if (ttid == 64) {
+            s_ticket[team][slot] = tk;
+            lds_release(&s_tkdone[team], it + 1u);
         }
         if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
@@ -1256,9 +1279,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
-            wait_ge(p, &s_rdone, it);
-            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
-            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
+            wait_ge(p, &s_rdone[team], it);
+            const uint32_t tf0 = uni(s_tfn[team][pslot][0]), tf1 = uni(s_tfn[team][pslot][1]);
+            const uint32_t tf2 = uni(s_tfn[team][pslot][2]), tf3 = uni(s_tfn[team][pslot][3]);
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, kTiming ? &bad : nullptr);
             if (lane == 0) {
                 const uint64_t end = O + (C ? tf3 : tf2);
@@ -1267,9 +1290,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     O = 0; C = 1;
                 }
                 // the other waves need only C and O: release them first, publish after
-                s_C[pslot] = C;
-                s_O[pslot] = O;
-                lds_release(&s_lbdone, it + 1u);
+                s_C[team][pslot] = C;
+                s_O[team][pslot] = O;
+                lds_release(&s_lbdone[team], it + 1u);
                 const uint64_t fin = O + (C ? tf3 : tf2);
                 if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
@@ -1295,22 +1318,22 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
         // T's bytes are consumed: the loads fly during the emission
         uint32_t Tn = kNone;
-        if (T < ntiles) {
-            wait_ge(p, &s_tkdone, it + 1u);
-            Tn = uni(s_ticket[slot]);
+        if (!kPf && T < ntiles) {
+            wait_ge(p, &s_tkdone[team], it + 1u);
+            Tn = uni(s_ticket[team][slot]);
             if (Tn >= ntiles) Tn = kNone;
         }
-        if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
+        if (!kPf && Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
         if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
-            wait_ge(p, &s_lbdone, it + 1u);
+            wait_ge(p, &s_lbdone[team], it + 1u);
             if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
 #if defined(BLT_EXP) && (BLT_EXP & 8)
             if (Tp == kNone - 1u)   // timing experiment: no emission
 #endif
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
-            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], uni(s_C[pslot]), uni64(s_O[pslot]),
-                      s_stage[wave]);
+            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[team][pslot], uni(s_C[team][pslot]), uni64(s_O[team][pslot]),
+                      s_stage[gw]);
             __builtin_amdgcn_s_setprio(0);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
@@ -1320,9 +1343,26 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
         }
-        if (stamping && tid == 0 && Tp < ntiles) {
+        if (stamping && ttid == 0 && Tp < ntiles) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
             e[2] = __builtin_amdgcn_s_memtime();
+        }
+        if (kPf) {
+            // T <- Tq (its bytes were loaded at this iteration's start), Tq <- the ticket claimed then
+            uint32_t Tr = kNone;
+            if (Tq < ntiles) {
+                wait_ge(p, &s_tkdone[team], it + 1u);
+                Tr = uni(s_ticket[team][slot]);
+                if (Tr >= ntiles) Tr = kNone;
+#pragma unroll
+                for (int j = 0; j < kS; ++j) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) x[j][q] = xq[j][q];
+                    nxt[j] = nxtq[j];
+                }
+            }
+            Tn = Tq;
+            Tq = Tr;
         }
         sp = sc;
         tip = ti;
