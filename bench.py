@@ -153,7 +153,7 @@ def main():
                        "parallelism": f"chunk-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "seg::scan_bytes_kernel<true>", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "seg::scan_bytes_kernel<true, true>", "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,

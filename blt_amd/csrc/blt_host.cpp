@@ -206,6 +206,9 @@ struct blt_bpe {
     // Self-token tables of the byte-pass kernel: entry (a, b) = merged token, or a itself when
     // (a, b) is no merge.  Usable when no byte-pair key (a, b) maps to a (self_ok).
     bool self_ok = true;
+    // Every byte-pair merge value is >= 256 (every merges file: ids 256 + line): the byte-pass
+    // kernel then reads "merge" off the entry's high byte instead of comparing it with a.
+    bool hi_merge = true;
     std::vector<uint16_t> self_ne, self_be;
     std::vector<uint64_t> hslots;          // general map, empty when single_pass
     uint64_t hmask = 0;
@@ -261,6 +264,7 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
         if (a < 256 && b < 256) {
             h->self_ne[blt::dense_index(a, b)] = kv.second;
             if (kv.second == a) h->self_ok = false;
+            if (kv.second < 256) h->hi_merge = false;
         }
     }
     h->self_be.resize(65536);
@@ -399,7 +403,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.hmask = h->hmask;
     p.cs_magic = cs ? ~0ull / cs : 0;
     p.debug = g_debug_tiles;
-    if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, dev, s));
+    if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }

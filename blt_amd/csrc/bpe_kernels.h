@@ -44,7 +44,8 @@ struct PassParams {
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);
 // Byte-input pass (segment kernel, seg::scan_bytes_kernel): p.cs >= kMinChunkBytes; tiles of
 // kTilePosBytes positions.
-hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int device, hipStream_t s);
+// hi_merge: every byte-pair merge value is >= 256, so an entry's high byte tells a merge.
+hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 

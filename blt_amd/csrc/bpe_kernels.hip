@@ -668,7 +668,7 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
 // ---- phase 1 of a tile: lookups, lane functions, wave functions ------------------------------
 // Three straight-line passes over the kS sub-tiles (lookups; the rare uniform fix-up of buffer
 // and chunk ends; lane functions and wave resolves), so the scheduler can overlap sub-tiles.
-template <bool kBE>
+template <bool kBE, bool kHiM>
 __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS][4], const uint32_t (&nxt)[kS],
                                             const TInfo& ti, uint32_t cs32, uint32_t wave, int lane,
                                             TileState& st, uint32_t (*wfn)[4]) {
@@ -688,18 +688,31 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
 #if defined(BLT_EXP) && (BLT_EXP & 1)
             st.v[j][h] = (t * 0x9E3779B1u) & 0xFF00FF00u;   // timing experiment: no LDS lookups
+#elif defined(BLT_EXP) && (BLT_EXP & 32)
+            // timing experiment: conflict-free lookups (lane l of a 32-lane group reads bank l)
+            const uint32_t cf = tab + 4u * (uint32_t)(lane & 31) + 128u * (uint32_t)h + (t & 0x7000u);
+            const uint32_t va = *(const lds_u16*)(uintptr_t)cf;
+            const uint32_t vb = *(const lds_u16*)(uintptr_t)(cf + 2u);
+            st.v[j][h] = va | (vb << 16);
 #else
             const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
             const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
-            st.v[j][h] = va | (vb << 16);
+            st.v[j][h] = __builtin_amdgcn_perm(vb, va, 0x05040100u);   // va | vb << 16, one op
 #endif
         }
         uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-            // token of a itself, in output byte order: BE (a << 8), native a
-            const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
-            m32 |= pk_nz(st.v[j][h] ^ self) << (2 * h);
+            uint32_t d;
+            if (kHiM) {
+                // a merge is a token >= 256, a itself < 256: the token's high byte (BE: low byte)
+                d = st.v[j][h] & (kBE ? 0x00FF00FFu : 0xFF00FF00u);
+            } else {
+                // token of a itself, in output byte order: BE (a << 8), native a
+                const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
+                d = st.v[j][h] ^ self;
+            }
+            m32 |= pk_nz(d) << (2 * h);
         }
         m[j] = (m32 & 0xFFFFu) | (m32 >> 15);
     }
@@ -978,6 +991,40 @@ __device__ __forceinline__ void stage_dense(const uint32_t (&v)[8], uint32_t c, 
     }
 }
 
+// Dense wave range straight from registers: lane l's 16-byte output block (see stage_dense) goes
+// to global memory with one buffer_store_b128, no LDS stage.  With the range 16-byte aligned
+// (rg = 0: every tile of a dense text emits a multiple of 8 tokens) that is the whole emission;
+// otherwise lane 0 stores the head of its block (its first 8 - rg/2 tokens) and lane 63 the block
+// after the range (its last rg/2 tokens) token by token.
+__device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, uint32_t rg, __amdgpu_buffer_rsrc_t ro,
+                                           uint32_t ab, int lane) {
+    const uint32_t sel = c ? 0x05040100u : 0x07060302u;   // low halves (c = 1) or high halves (c = 0)
+    u32x4 P;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
+    const uint32_t o = ab + 16u * (uint32_t)lane;
+    if (rg == 0) {
+        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, 0);
+        return;
+    }
+    u32x4 Q;   // lane l - 1's tokens
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
+    const uint32_t off = 16u - rg;
+    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, 0);
+    if (lane == 0 || lane == 63) {
+        const uint32_t h = 8u - (rg >> 1);   // tokens of this lane in its own block
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint16_t tok = (uint16_t)(P[k >> 1] >> (16 * (k & 1)));
+            if (lane == 0 && (uint32_t)k < h) __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, 0);
+            if (lane == 63 && (uint32_t)k >= h)
+                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 1024u + 2u * (k - h)), 0, 0);
+        }
+    }
+}
+
 // ---- emission of the pending tile --------------------------------------------------------
 // Tile-level: carry-in C, O tokens before the tile; the output resource starts at the 16-byte
 // boundary at or below byte 2 O, so every offset below is 32-bit.
@@ -1015,6 +1062,12 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
             if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
+#if !defined(BLT_DD) || BLT_DD
+        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {       // dense: every pair merges, no buffer end
+            emit_dense(st.v[j], cg, rg, ro, ab, lane);
+            continue;
+        }
+#endif
         if (rg + 2u * wcnt > (uint32_t)kStageWave) {
             // rare (few merges): each landed token straight to global memory
             uint32_t o = gb + 2u * lane_off;
@@ -1139,6 +1192,23 @@ constexpr bool kPf = BLT_PF != 0;
 #else
 constexpr bool kPf = false;
 #endif
+// Ticket distance: kTk2 claims the tile after next at the start of each iteration (a whole
+// iteration for the device-scope atomic to return); kPf implies it.
+#ifdef BLT_TK2
+constexpr bool kTk2 = kPf || BLT_TK2 != 0;
+#else
+constexpr bool kTk2 = kPf;
+#endif
+// kTkN: the ticket claimed at the start of an iteration is handed to the other waves at the start
+// of the next one (a whole iteration for the atomic to return, so the claiming wave never waits
+// for it) and names the tile loaded after that iteration's phase 1.  Needs the atomic optimizer
+// off (-mllvm -amdgpu-atomic-optimizer-strategy=None): its wave-aggregated form waits for the
+// atomic right where it is issued.
+#ifdef BLT_TKN
+constexpr bool kTkN = !kTk2 && BLT_TKN != 0;
+#else
+constexpr bool kTkN = false;
+#endif
 
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
     return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1158,7 +1228,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
     }
 }
 
-template <bool kBE>
+template <bool kBE, bool kHiM>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kAllWaves][kStageWave];
@@ -1192,9 +1262,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         s_ticket[team][0] = atomicAdd(p.ctl, 1u);
 #endif
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (kPf) s_ticket[team][1] = s_ticket[team][0] + gridDim.x * kTeams;
+        if (kTk2) s_ticket[team][1] = s_ticket[team][0] + gridDim.x * kTeams;
 #else
-        if (kPf) s_ticket[team][1] = atomicAdd(p.ctl, 1u);   // the tile after it (prefetched in iteration 0)
+        if (kTk2) s_ticket[team][1] = atomicAdd(p.ctl, 1u);   // the tile after it
+        if (kTkN) s_ticket[team][kRing - 1] = atomicAdd(p.ctl, 1u);   // read in iteration 0
 #endif
         for (int r = 0; r < kRing; ++r) s_p1cnt[team][r] = 0;
         s_rdone[team] = 0; s_lbdone[team] = 0; s_tkdone[team] = 0;
@@ -1206,10 +1277,38 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
+#if defined(BLT_EXP) && (BLT_EXP & 4096)
+    {   // timing experiment: phase 1 alone over static tiles (bytes prefetched one tile ahead)
+        uint32_t xa[kS][4], na[kS], xb[kS][4], nb[kS];
+        TileState st;
+        uint32_t acc = 0, it = 0;
+        uint32_t Ta = blockIdx.x;
+        if (Ta < ntiles) load_tile(p, Ta, wave, lane, xa, na);
+        for (; Ta < ntiles; Ta += 2 * gridDim.x) {
+            const uint32_t Tb = Ta + gridDim.x;
+#if BLT_EXP & 8192   // compute only: every tile reuses the first tile's bytes
+            if (Ta == blockIdx.x && Tb < ntiles) load_tile(p, Ta, wave, lane, xb, nb);
+#else
+            if (Tb < ntiles) load_tile(p, Tb, wave, lane, xb, nb);
+#endif
+            phase1_tile<kBE, kHiM>(tab, xa, na, tile_info(p, Ta), cs32, wave, lane, st, s_wfn[0][(it++) & 3]);
+            acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
+            if (Tb >= ntiles) break;
+            const uint32_t Tc = Tb + gridDim.x;
+#if !(BLT_EXP & 8192)
+            if (Tc < ntiles) load_tile(p, Tc, wave, lane, xa, na);
+#endif
+            phase1_tile<kBE, kHiM>(tab, xb, nb, tile_info(p, Tb), cs32, wave, lane, st, s_wfn[0][(it++) & 3]);
+            acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
+        }
+        if (acc == 0x9E3779B9u) p.ctl[15] = acc;
+        return;
+    }
+#endif
     uint32_t T = uni(s_ticket[team][0]);    // tile in phase 1
     uint32_t Tp = kNone;              // tile waiting for emission
-    uint32_t Tq = kNone;              // kPf: the tile after T (its bytes are loaded during T's iteration)
-    if (kPf) { Tq = uni(s_ticket[team][1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
+    uint32_t Tq = kNone;              // kTk2: the tile after T (kPf: its bytes are loaded during T's iteration)
+    if (kTk2) { Tq = uni(s_ticket[team][1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
     __syncthreads();
 
     uint32_t x[kS][4];      // input bytes of each sub-tile of T
@@ -1221,6 +1320,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     if (T < ntiles) ti = tile_info(p, T);
     TileState sp, sc;       // phase-1 state of Tp (pending) and of T (current)
     uint64_t lbs[kLbWin];   // wave 0: status words for the pending tile's look-back
+    uint32_t tkc = kNone;   // kTkN, claiming lane: the ticket claimed in the previous iteration
 
     for (uint32_t it = 0; T < ntiles || Tp < ntiles; ++it) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
@@ -1234,10 +1334,17 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
+        if (kTkN && ttid == 64) {
+            if (it > 0) {
+                s_ticket[team][pslot] = tkc;
+                lds_release(&s_tkdone[team], it);
+            }
+            tkc = T < ntiles ? atomicAdd(p.ctl, 1u) : kNone;
+        }
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (ttid == 64 && (kPf ? Tq : T) < ntiles) tk = (kPf ? Tq : T) + gridDim.x * kTeams;
+        if (ttid == 64 && (kTk2 ? Tq : T) < ntiles) tk = (kTk2 ? Tq : T) + gridDim.x * kTeams;
 #else
-        if (ttid == 64 && (kPf ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (!kTkN && ttid == 64 && (kTk2 ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
 #endif
         asm volatile("" ::: "memory");
 
@@ -1251,7 +1358,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tile<kBE>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[team][slot]);
+            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[team][slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
@@ -1264,7 +1371,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        if (ttid == 64) {
+        if (!kTkN && ttid == 64) {
             s_ticket[team][slot] = tk;
             lds_release(&s_tkdone[team], it + 1u);
         }
@@ -1318,11 +1425,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
         // T's bytes are consumed: the loads fly during the emission
         uint32_t Tn = kNone;
-        if (!kPf && T < ntiles) {
-            wait_ge(p, &s_tkdone[team], it + 1u);
-            Tn = uni(s_ticket[team][slot]);
+        if (!kTk2 && T < ntiles) {
+            wait_ge(p, &s_tkdone[team], kTkN ? it : it + 1u);
+            Tn = uni(s_ticket[team][kTkN ? pslot : slot]);
             if (Tn >= ntiles) Tn = kNone;
         }
+        if (kTk2 && !kPf) Tn = Tq;
         if (!kPf && Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
         if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
@@ -1347,18 +1455,20 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
             e[2] = __builtin_amdgcn_s_memtime();
         }
-        if (kPf) {
-            // T <- Tq (its bytes were loaded at this iteration's start), Tq <- the ticket claimed then
+        if (kTk2) {
+            // Tq <- the ticket claimed at this iteration's start; kPf: T <- Tq's bytes, loaded then
             uint32_t Tr = kNone;
             if (Tq < ntiles) {
                 wait_ge(p, &s_tkdone[team], it + 1u);
                 Tr = uni(s_ticket[team][slot]);
                 if (Tr >= ntiles) Tr = kNone;
+                if (kPf) {
 #pragma unroll
-                for (int j = 0; j < kS; ++j) {
+                    for (int j = 0; j < kS; ++j) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) x[j][q] = xq[j][q];
-                    nxt[j] = nxtq[j];
+                        for (int q = 0; q < 4; ++q) x[j][q] = xq[j][q];
+                        nxt[j] = nxtq[j];
+                    }
                 }
             }
             Tn = Tq;
@@ -1449,17 +1559,26 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
     return hipGetLastError();
 }
 
-hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int device, hipStream_t s) {
+hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s) {
     if (p.ntiles == 0) return hipSuccess;
-    const void* fn = big_endian ? (const void*)seg::scan_bytes_kernel<true> : (const void*)seg::scan_bytes_kernel<false>;
+    const void* fn = big_endian ? (hi_merge ? (const void*)seg::scan_bytes_kernel<true, true>
+                                            : (const void*)seg::scan_bytes_kernel<true, false>)
+                                : (hi_merge ? (const void*)seg::scan_bytes_kernel<false, true>
+                                            : (const void*)seg::scan_bytes_kernel<false, false>);
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, seg::kThreads, 0) != hipSuccess || occ < 1) occ = 1;
     long long grid = (long long)(cus > 0 ? cus : 1) * occ;
     if (grid > (long long)p.ntiles) grid = p.ntiles;
-    if (big_endian) hipLaunchKernelGGL(seg::scan_bytes_kernel<true>, dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
-    else hipLaunchKernelGGL(seg::scan_bytes_kernel<false>, dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
+    const dim3 g((unsigned)grid), b(seg::kThreads);
+    if (big_endian) {
+        if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<true, true>), g, b, 0, s, p);
+        else hipLaunchKernelGGL((seg::scan_bytes_kernel<true, false>), g, b, 0, s, p);
+    } else {
+        if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<false, true>), g, b, 0, s, p);
+        else hipLaunchKernelGGL((seg::scan_bytes_kernel<false, false>), g, b, 0, s, p);
+    }
     return hipGetLastError();
 }
 

@@ -106,6 +106,21 @@ def test_general_maps_multipass():
         assert got == _oracle_chunk(m, data), (trial, m)
 
 
+@pytest.mark.parametrize("cs", [4096, 65536, 1 << 20])
+def test_byte_valued_single_pass(cs):
+    """Merge values below 256 that are no key component (tokenizer.rs:283-291 style): one pass,
+    on the byte-pass kernel's self-compare form (an entry's high byte does not tell a merge)."""
+    rng = np.random.default_rng(cs)
+    m = {(a, b): 200 + ((a * 7 + b) % 50) for a in range(97, 123) for b in range(97, 123) if (a + b) % 3}
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is True
+    data = rng.integers(97, 123, 3 * (1 << 20) + 5, dtype=np.uint8)
+    got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
+
+
 def test_chained_map_long():
     m = {(97, 97): 97}  # "aa" -> "a": log2(n) passes
     data = b"a" * 100000 + b"b" + b"a" * 3
