@@ -630,6 +630,12 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
     v += dpp0<0x143, 0xC>(v);
     return v;
 }
+// mask's bit for this lane ? if1 : if0, one v_cndmask on the SGPR lane mask
+__device__ __forceinline__ uint32_t lane_sel(uint64_t mask, uint32_t if0, uint32_t if1) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(mask));
+    return r;
+}
 __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int i) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
 }
@@ -772,11 +778,11 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
         const uint64_t F = nonid ? ((nonid & (0ull - nonid)) << 1) - 1ull : ~0ull;
         const uint64_t CI0 = Y, CI1 = Y | F;
-        const uint32_t c0 = (uint32_t)(CI0 >> lane) & 1u, c1 = (uint32_t)(CI1 >> lane) & 1u;
-        const uint32_t packed = (c0 ? cnt1 : cnt0) | ((c1 ? cnt1 : cnt0) << 16);
+        // per lane: count under its carry-in, for wave carry-in 0 (low half) and 1 (high half)
+        const uint32_t packed = lane_sel(CI0, cnt0, cnt1) | (lane_sel(CI1, cnt0, cnt1) << 16);
         const uint32_t incl = wave_scan(packed);
         st.ex[j] = incl - packed;
-        st.lw[j] = c0 | (c1 << 1);   // this lane's carry-in for wave carry-in 0 | 1
+        st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
         if (lane == 63) {
             const uint32_t g = (uint32_t)j * kWaves + wave;
             wfn[g][0] = nonid == 0;
@@ -1045,6 +1051,20 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
         const uint32_t cg = uni(gin[g][C]);
         const uint32_t goff = uni(gin[g][2 + C]);          // tokens before this wave range in the tile
+        const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
+        const uint32_t ab = gb & ~15u, rg = gb - ab;
+        // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
+        while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
+        const bool cstart = p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos;
+#if !defined(BLT_DD) || BLT_DD
+        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
+            // dense: every pair merges, no buffer end, so no chunk end: a chunk can only start at
+            // the range's first position
+            if (cstart && lane == 0) p.chunk_off[kc] = O + goff;
+            emit_dense(st.v[j], cg, rg, ro, ab, lane);
+            continue;
+        }
+#endif
         const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
         const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
         const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
@@ -1054,20 +1074,10 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
         const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
         const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
-        const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
-        const uint32_t ab = gb & ~15u, rg = gb - ab;
-        // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
-        while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
-        if (p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos) {
+        if (cstart) {
             const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
             if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
-#if !defined(BLT_DD) || BLT_DD
-        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {       // dense: every pair merges, no buffer end
-            emit_dense(st.v[j], cg, rg, ro, ab, lane);
-            continue;
-        }
-#endif
         if (rg + 2u * wcnt > (uint32_t)kStageWave) {
             // rare (few merges): each landed token straight to global memory
             uint32_t o = gb + 2u * lane_off;
@@ -1186,11 +1196,12 @@ constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
 constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
 #endif
 // Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
-// iteration (a whole iteration to land) and claims tickets two tiles ahead.
+// iteration (a whole iteration to land) and claims tickets two tiles ahead (default; BLT_PF=0
+// loads each tile after the previous tile's phase 1).
 #ifdef BLT_PF
 constexpr bool kPf = BLT_PF != 0;
 #else
-constexpr bool kPf = false;
+constexpr bool kPf = true;
 #endif
 // Ticket distance: kTk2 claims the tile after next at the start of each iteration (a whole
 // iteration for the device-scope atomic to return); kPf implies it.
@@ -1208,6 +1219,13 @@ constexpr bool kTk2 = kPf;
 constexpr bool kTkN = !kTk2 && BLT_TKN != 0;
 #else
 constexpr bool kTkN = false;
+#endif
+// kLbe: wave 0 issues the pending tile's look-back loads at the start of the iteration (they fly
+// during its phase 1) instead of the first wave to finish phase 1 issuing them after it.
+#ifdef BLT_LBE
+constexpr bool kLbe = BLT_LBE != 0;
+#else
+constexpr bool kLbe = false;
 #endif
 
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
@@ -1277,6 +1295,31 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
+#if defined(BLT_EXP) && (BLT_EXP & 16384)
+    {   // timing experiment: the memory traffic alone (read a tile, write 32 KiB), static tiles,
+        // the next tile's bytes prefetched one tile ahead
+        uint32_t xa[kS][4], na[kS];
+        const __amdgpu_buffer_rsrc_t ro = rsrc_at(p.out, p.out_cap);
+        uint32_t Ta = blockIdx.x;
+        if (Ta < ntiles) load_tile(p, Ta, wave, lane, xa, na);
+        for (; Ta < ntiles; Ta += gridDim.x) {
+            uint32_t xb[kS][4];
+#pragma unroll
+            for (int j = 0; j < kS; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) xb[j][q] = xa[j][q] ^ na[j];
+            const uint32_t Tb = Ta + gridDim.x;
+            if (Tb < ntiles) load_tile(p, Tb, wave, lane, xa, na);
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+                const u32x4 v = {xb[j][0], xb[j][1], xb[j][2], xb[j][3]};
+                const uint32_t o = (uint32_t)(Ta % 16384u) * 32768u + (uint32_t)j * 16384u + wave * 1024u + 16u * lane;
+                __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)o, 0, 0);
+            }
+        }
+        return;
+    }
+#endif
 #if defined(BLT_EXP) && (BLT_EXP & 4096)
     {   // timing experiment: phase 1 alone over static tiles (bytes prefetched one tile ahead)
         uint32_t xa[kS][4], na[kS], xb[kS][4], nb[kS];
@@ -1330,6 +1373,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
         if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
+        if (kLbe && wave == 0 && Tp < ntiles && Tp > 0) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
@@ -1364,14 +1408,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[team][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
-            lbw = old == (uint32_t)kWaves * (it / kRing);
+            lbw = kLbe ? wave == 0 : old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[team][slot], s_gin[team][slot], s_tfn[team][slot]);
                 if (lane == 0) lds_release(&s_rdone[team], it + 1u);
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        if (!kTkN && ttid == 64) {
+        if (!kTkN && !kTk2 && ttid == 64) {
             s_ticket[team][slot] = tk;
             lds_release(&s_tkdone[team], it + 1u);
         }
@@ -1383,7 +1427,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
-            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            if (lb && !kLbe) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone[team], it);
@@ -1456,7 +1500,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             e[2] = __builtin_amdgcn_s_memtime();
         }
         if (kTk2) {
-            // Tq <- the ticket claimed at this iteration's start; kPf: T <- Tq's bytes, loaded then
+            // Tq <- the ticket claimed at this iteration's start (handed over after the claiming
+            // wave's emission: a whole iteration for the atomic); kPf: T <- Tq's bytes, loaded then
+            if (ttid == 64) {
+                s_ticket[team][slot] = tk;
+                lds_release(&s_tkdone[team], it + 1u);
+            }
             uint32_t Tr = kNone;
             if (Tq < ntiles) {
                 wait_ge(p, &s_tkdone[team], it + 1u);
