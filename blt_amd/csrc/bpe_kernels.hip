@@ -566,10 +566,14 @@ constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
 // Per-wave token stage: a wave range of 1024 positions emits 512..1024 tokens; the stage holds
-// 521 (2-byte aligned start + up to 1042 bytes) — every range of a text whose pairs mostly merge.
-// A range with more tokens stores them straight to global memory (emit_direct).
+// 521 (2-byte aligned start + up to 1042 bytes).  A range with more tokens goes through it in two
+// parts of 32 lanes (at most 512 tokens each).
 constexpr int kStageWave = 1056;
+#ifdef BLT_LBWIN
+constexpr int kLbWin = BLT_LBWIN;                      // look-back windows of 64 per round trip
+#else
 constexpr int kLbWin = 1;                              // look-back windows of 64 per round trip
+#endif
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
@@ -756,7 +760,11 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             st.mv[j] = m[j] | 0xFFFF0000u;
         }
     }
-    // lane functions (both carry-in hypotheses, packed 16-bit) and wave resolves
+    // lane functions (both carry-in hypotheses, packed 16-bit) and wave resolves; the sub-tiles'
+    // dependency chains (ballots, SGPR carry chain, DPP scan) sit in one basic block so they
+    // interleave, and lane 63 writes both wave functions after them
+    uint64_t wnonid[kS], wcmask[kS];
+    uint32_t wincl[kS];
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t vm = st.mv[j] >> 16;
@@ -783,12 +791,19 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         const uint32_t incl = wave_scan(packed);
         st.ex[j] = incl - packed;
         st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
-        if (lane == 63) {
+        wnonid[j] = nonid;
+        wcmask[j] = cmask;
+        wincl[j] = incl;
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
             const uint32_t g = (uint32_t)j * kWaves + wave;
+            const uint64_t nonid = wnonid[j];
             wfn[g][0] = nonid == 0;
-            wfn[g][1] = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
-            wfn[g][2] = incl & 0xFFFFu;
-            wfn[g][3] = incl >> 16;
+            wfn[g][1] = nonid ? (uint32_t)((wcmask[j] >> (63 - __clzll(nonid))) & 1ull) : 0u;
+            wfn[g][2] = wincl[j] & 0xFFFFu;
+            wfn[g][3] = wincl[j] >> 16;
         }
     }
 }
@@ -954,10 +969,9 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
 // Every pair of a wave range merges (text under a large merge map): every lane is an identity
 // function, so all lanes take the wave's carry-in c and emit exactly 8 tokens - the low halves
 // of v (c = 1, positions 0, 2, .., 14) or the high halves (c = 0, positions 1, 3, .., 15).  A lane
-// packs them into 16 bytes; the stage places token n of the range at byte rg + 2n, so the aligned
-// 16-byte block l holds the last rg/2 tokens of lane l-1 and the first 8 - rg/2 of lane l: one
-// DPP fetch, a funnel shift and one conflict-free ds_write_b128 per lane (lane 63 also writes the
-// block after the range).  Bytes of block 0 before rg are garbage the copy-out never reads.
+// packs them into 16 bytes.  Token n of the range goes to output byte rg + 2n past the 16-byte
+// boundary ab, so the aligned block l holds the last rg/2 tokens of lane l-1 and the first
+// 8 - rg/2 of lane l: one DPP fetch and a funnel shift per lane.
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
     return r ? __builtin_amdgcn_alignbyte(hi, lo, 2) : lo;   // r in {0, 2}
 }
@@ -975,29 +989,7 @@ __device__ __forceinline__ u32x4 block_of(const u32x4& a, const u32x4& b, uint32
     }
     return o;
 }
-__device__ __forceinline__ void stage_dense(const uint32_t (&v)[8], uint32_t c, uint32_t rg, uint32_t stg_lds, int lane) {
-    const uint32_t sel = c ? 0x05040100u : 0x07060302u;   // low halves (c = 1) or high halves (c = 0)
-    u32x4 P;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
-    if (rg == 0) {
-        *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * (uint32_t)lane) = P;
-        return;
-    }
-    u32x4 Q;   // lane l - 1's tokens (lane 0: garbage, lands before rg)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
-    const uint32_t off = 16u - rg;   // block l = bytes [16 - rg, 32 - rg) of Q ++ P
-    const uint32_t d = off >> 2, r = off & 3u;
-    *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * (uint32_t)lane) = block_of(Q, P, d, r);
-    if (lane == 63) {   // block 64: lane 63's last rg / 2 tokens
-        const u32x4 z = {0u, 0u, 0u, 0u};
-        *(__attribute__((address_space(3))) u32x4*)(uintptr_t)(stg_lds + 16u * 64u) = block_of(P, z, d, r);
-    }
-}
-
-// Dense wave range straight from registers: lane l's 16-byte output block (see stage_dense) goes
+// Dense wave range straight from registers: lane l's 16-byte output block goes
 // to global memory with one buffer_store_b128, no LDS stage.  With the range 16-byte aligned
 // (rg = 0: every tile of a dense text emits a multiple of 8 tokens) that is the whole emission;
 // otherwise lane 0 stores the head of its block (its first 8 - rg/2 tokens) and lane 63 the block
@@ -1056,7 +1048,6 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
         while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
         const bool cstart = p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos;
-#if !defined(BLT_DD) || BLT_DD
         if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
             // dense: every pair merges, no buffer end, so no chunk end: a chunk can only start at
             // the range's first position
@@ -1064,7 +1055,6 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             emit_dense(st.v[j], cg, rg, ro, ab, lane);
             continue;
         }
-#endif
         const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
         const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
         const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
@@ -1078,54 +1068,51 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
             if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
-        if (rg + 2u * wcnt > (uint32_t)kStageWave) {
-            // rare (few merges): each landed token straight to global memory
-            uint32_t o = gb + 2u * lane_off;
+        // Stage -> global in one part, or in two (lanes 0..31, then 32..63: at most 512 tokens
+        // each) when the range's tokens overflow the stage (few merges, e.g. random bytes).
+        const uint32_t two = rg + 2u * wcnt > (uint32_t)kStageWave ? 1u : 0u;
+        const uint32_t off32 = two ? uni(lane_u32(lane_off, 32)) : 0u;   // tokens before lane 32
+        for (uint32_t part = 0; part <= two; ++part) {
+            const uint32_t base = part ? off32 : 0u;
+            const uint32_t cnt = two ? (part ? wcnt - off32 : off32) : wcnt;
+            const uint32_t gbp = gb + 2u * base, abp = gbp & ~15u, rgp = gbp - abp;
+            if (!two || ((uint32_t)lane >> 5) == part) {
+                uint32_t a = stg_lds + rgp + 2u * (lane_off - base);   // LDS byte address of the next token
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                if ((L >> k) & 1u) {
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(st.v[j][k >> 1] >> (16 * (k & 1))), ro, (int)o, 0, 0);
-                    o += 2u;
+                for (int h = 0; h < 8; ++h) {
+                    const uint32_t tok = st.v[j][h];
+#if defined(BLT_EXP) && (BLT_EXP & 2)
+                    asm volatile("" :: "v"(tok), "v"(a));   // timing experiment: no stage stores
+                    add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+                    if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+#else
+                    // a consumed position writes the slot the next landing token overwrites
+                    *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
+                    add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+                    if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
+                    if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+#endif
                 }
             }
-            continue;
-        }
-        uint32_t a = stg_lds + rg + 2u * lane_off;          // LDS byte address of this lane's next token
-        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {       // dense: every pair merges, no buffer end
-            stage_dense(st.v[j], cg, rg, stg_lds, lane);
-        } else
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            const uint32_t tok = st.v[j][h];
-#if defined(BLT_EXP) && (BLT_EXP & 2)
-            asm volatile("" :: "v"(tok), "v"(a));           // timing experiment: no stage stores
-            add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
-            if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
-#else
-            *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
-            add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
-            if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
-            if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
-#endif
-        }
-        // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each,
-        // lanes 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order queue).
-        const uint32_t re = rg + 2u * wcnt;
-        const uint32_t hend = ((rg + 15u) & ~15u) < re ? ((rg + 15u) & ~15u) : re;
-        const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
-        const uint32_t nfull = (tbeg - hend) >> 4;
+            // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each,
+            // lanes 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order queue).
+            const uint32_t re = rgp + 2u * cnt;
+            const uint32_t hend = ((rgp + 15u) & ~15u) < re ? ((rgp + 15u) & ~15u) : re;
+            const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
+            const uint32_t nfull = (tbeg - hend) >> 4;
 #if defined(BLT_EXP) && (BLT_EXP & 4)
-        if (nfull == 12345u)   // timing experiment: no copy-out
+            if (nfull == 12345u)   // timing experiment: no copy-out
 #endif
-        for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
-            const uint32_t o = hend + 16u * i;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(stg + o);
-            __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)(ab + o), 0, 0);
-        }
-        if (lane < 16) {
-            const uint32_t o = lane < 8 ? rg + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
-            const uint32_t lim = lane < 8 ? hend : re;
-            if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)(ab + o), 0, 0);
+            for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
+                const uint32_t o = hend + 16u * i;
+                const u32x4 v = *reinterpret_cast<const u32x4*>(stg + o);
+                __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)(abp + o), 0, 0);
+            }
+            if (lane < 16) {
+                const uint32_t o = lane < 8 ? rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+                const uint32_t lim = lane < 8 ? hend : re;
+                if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)(abp + o), 0, 0);
+            }
         }
     }
 }
@@ -1219,6 +1206,23 @@ constexpr bool kTk2 = kPf;
 constexpr bool kTkN = !kTk2 && BLT_TKN != 0;
 #else
 constexpr bool kTkN = false;
+#endif
+// kLead: wave 0 runs phase 1 at the top priority and always takes the look-back (it finishes
+// phase 1 well before the others, so its look-back round trip overlaps their phase 1).
+#ifdef BLT_LEAD
+constexpr bool kLead = BLT_LEAD != 0;
+#else
+constexpr bool kLead = false;
+#endif
+// kP3: three-stage pipeline.  Iteration i runs phase 1 of T_i; wave 0 issues the look-back loads
+// of T_{i-1}; every wave emits T_{i-2} (its carry-in and offset are known since the end of the
+// last iteration); then wave 0 folds T_{i-1}'s look-back, its loads having flown during the
+// emission, and publishes T_{i-1}'s inclusive prefix while the other waves start the next
+// phase 1.  Needs !kPf (registers).
+#ifdef BLT_P3
+constexpr bool kP3 = BLT_P3 != 0;
+#else
+constexpr bool kP3 = false;
 #endif
 // kLbe: wave 0 issues the pending tile's look-back loads at the start of the iteration (they fly
 // during its phase 1) instead of the first wave to finish phase 1 issuing them after it.
@@ -1348,6 +1352,115 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         return;
     }
 #endif
+    if constexpr (kP3) {
+        static_assert(!kPf && !kTk2 && !kTkN && kTeams == 1, "three-stage pipeline: one team, no prefetch");
+        uint32_t T = uni(s_ticket[0][0]);
+        uint32_t Tp = kNone, Tpp = kNone;   // look-back in flight; emission this iteration
+        uint32_t x[kS][4], nxt[kS];
+        if (T < ntiles) load_tile(p, T, wave, lane, x, nxt);
+        TInfo ti = {}, tip = {}, tipp = {};
+        if (T < ntiles) ti = tile_info(p, T);
+        TileState spp, sp, sc;
+        uint64_t lbs[kLbWin];
+        for (uint32_t it = 0; T < ntiles || Tp < ntiles || Tpp < ntiles; ++it) {
+            const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1), ppslot = (it - 2) & (kRing - 1);
+            uint64_t stamp[7];
+            const bool stamping = kTiming && p.debug != nullptr;
+            if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
+            if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
+            uint32_t tk = kNone;
+            if (tid == 64 && T < ntiles) tk = atomicAdd(p.ctl, 1u);
+            asm volatile("" ::: "memory");
+            if (T < ntiles) {
+                if (wave == 0) __builtin_amdgcn_s_setprio(3);
+                else if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+                phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[0][slot]);
+                __builtin_amdgcn_s_setprio(0);
+                uint32_t old = 0;
+                if (lane == 0)
+                    old = __hip_atomic_fetch_add(&s_p1cnt[0][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = uni(old);
+                if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
+                    resolve_tile(p, T, lane, s_wfn[0][slot], s_gin[0][slot], s_tfn[0][slot]);
+                    if (lane == 0) lds_release(&s_rdone[0], it + 1u);
+                }
+            }
+            if (tid == 64) {
+                s_ticket[0][slot] = tk;
+                lds_release(&s_tkdone[0], it + 1u);
+            }
+            if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
+            if (wave == 0 && Tp < ntiles && Tp > 0) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            uint32_t Tn = kNone;
+            if (T < ntiles) {
+                wait_ge(p, &s_tkdone[0], it + 1u);
+                Tn = uni(s_ticket[0][slot]);
+                if (Tn >= ntiles) Tn = kNone;
+            }
+            if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
+            if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
+            stamp[4] = stamp[3];
+            if (Tpp < ntiles) {
+                wait_ge(p, &s_lbdone[0], it);   // released at the end of the last iteration
+                if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
+                if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
+                emit_tile(p, Tpp, tipp, cs32, wave, lane, spp, s_gin[0][ppslot], uni(s_C[0][ppslot]),
+                          uni64(s_O[0][ppslot]), s_stage[gw]);
+                __builtin_amdgcn_s_setprio(0);
+            }
+            if (wave == 0) {
+                if (Tp < ntiles) {   // fold Tp's look-back: its loads flew during the emission
+                    uint32_t C = 1u, how = 0xFFFFu, spins = 0;
+                    uint64_t O = 0ull;
+                    if (Tp > 0) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+                    wait_ge(p, &s_rdone[0], it);   // Tp was resolved in iteration it - 1
+                    const uint32_t tf0 = uni(s_tfn[0][pslot][0]), tf1 = uni(s_tfn[0][pslot][1]);
+                    const uint32_t tf2 = uni(s_tfn[0][pslot][2]), tf3 = uni(s_tfn[0][pslot][3]);
+                    if (lane == 0) {
+                        const uint64_t end = O + (C ? tf3 : tf2);
+                        if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
+                            record_error(p, 4u, Tp, 0xFFu, O, end, C);
+                            O = 0; C = 1;
+                        }
+                        s_C[0][pslot] = C;
+                        s_O[0][pslot] = O;
+                        lds_release(&s_lbdone[0], it + 1u);
+                        const uint64_t fin = O + (C ? tf3 : tf2);
+                        if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
+                        if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
+                        if (Tp == ntiles - 1) {
+                            *p.total = fin;
+                            if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
+                        }
+                        if (p.debug) {
+                            uint64_t* d = p.debug + 4ull * Tp;
+                            d[0] = O;
+                            d[1] = ((uint64_t)C << 32) | how;
+                            d[2] = ((uint64_t)tf3 << 32) | tf2;
+                            d[3] = ((uint64_t)tf1 << 32) | tf0;
+                        }
+                    }
+                }
+            }
+            if (stamping && Tpp < ntiles && lane == 0) {
+                stamp[5] = __builtin_amdgcn_s_memtime();
+                stamp[6] = stamp[5];
+                uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tpp * kWaves + wave);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
+            }
+            spp = sp;
+            sp = sc;
+            tipp = tip;
+            tip = ti;
+            if (Tn < ntiles) ti = tile_info(p, Tn);
+            Tpp = Tp;
+            Tp = T;
+            T = Tn;
+        }
+        return;
+    }
     uint32_t T = uni(s_ticket[team][0]);    // tile in phase 1
     uint32_t Tp = kNone;              // tile waiting for emission
     uint32_t Tq = kNone;              // kTk2: the tile after T (kPf: its bytes are loaded during T's iteration)
@@ -1401,14 +1514,15 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // issue priority by age: the youngest waves lose the arbiter to the older ones, finish
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
-            if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+            if (kLead && wave == 0) __builtin_amdgcn_s_setprio(3);
+            else if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
             phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[team][slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[team][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
-            lbw = kLbe ? wave == 0 : old == (uint32_t)kWaves * (it / kRing);
+            lbw = (kLbe || kLead) ? wave == 0 : old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[team][slot], s_gin[team][slot], s_tfn[team][slot]);
                 if (lane == 0) lds_release(&s_rdone[team], it + 1u);
