@@ -7,11 +7,7 @@ namespace blt {
 
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
-// Byte-pass workgroups run BLT_TEAMS independent teams of waves, each with its own tile stream.
-#ifndef BLT_TEAMS
-#define BLT_TEAMS 1
-#endif
-constexpr uint64_t kTilePosBytes = 32768 / BLT_TEAMS;   // positions per look-back tile of the byte-input pass
+constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 

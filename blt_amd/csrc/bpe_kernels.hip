@@ -558,9 +558,7 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
 }
 
 constexpr int kThreads = 1024;                         // 16 waves: 4 per SIMD hide LDS and VALU latency
-constexpr int kTeams = BLT_TEAMS;                      // independent tile streams per workgroup
-constexpr int kAllWaves = kThreads / 64;
-constexpr int kWaves = kAllWaves / kTeams;             // waves per team: the tile geometry
+constexpr int kWaves = kThreads / 64;
 constexpr int kS = 2;                                  // sub-tiles per tile
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
@@ -1197,41 +1195,6 @@ constexpr bool kTk2 = kPf || BLT_TK2 != 0;
 #else
 constexpr bool kTk2 = kPf;
 #endif
-// kTkN: the ticket claimed at the start of an iteration is handed to the other waves at the start
-// of the next one (a whole iteration for the atomic to return, so the claiming wave never waits
-// for it) and names the tile loaded after that iteration's phase 1.  Needs the atomic optimizer
-// off (-mllvm -amdgpu-atomic-optimizer-strategy=None): its wave-aggregated form waits for the
-// atomic right where it is issued.
-#ifdef BLT_TKN
-constexpr bool kTkN = !kTk2 && BLT_TKN != 0;
-#else
-constexpr bool kTkN = false;
-#endif
-// kLead: wave 0 runs phase 1 at the top priority and always takes the look-back (it finishes
-// phase 1 well before the others, so its look-back round trip overlaps their phase 1).
-#ifdef BLT_LEAD
-constexpr bool kLead = BLT_LEAD != 0;
-#else
-constexpr bool kLead = false;
-#endif
-// kP3: three-stage pipeline.  Iteration i runs phase 1 of T_i; wave 0 issues the look-back loads
-// of T_{i-1}; every wave emits T_{i-2} (its carry-in and offset are known since the end of the
-// last iteration); then wave 0 folds T_{i-1}'s look-back, its loads having flown during the
-// emission, and publishes T_{i-1}'s inclusive prefix while the other waves start the next
-// phase 1.  Needs !kPf (registers).
-#ifdef BLT_P3
-constexpr bool kP3 = BLT_P3 != 0;
-#else
-constexpr bool kP3 = false;
-#endif
-// kLbe: wave 0 issues the pending tile's look-back loads at the start of the iteration (they fly
-// during its phase 1) instead of the first wave to finish phase 1 issuing them after it.
-#ifdef BLT_LBE
-constexpr bool kLbe = BLT_LBE != 0;
-#else
-constexpr bool kLbe = false;
-#endif
-
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
     return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1253,44 +1216,39 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
 template <bool kBE, bool kHiM>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kAllWaves][kStageWave];
-    // per team:
-    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kTeams][kRing][kGroups][4];   // wave functions (phase 1)
-    __shared__ uint32_t s_gin[kTeams][kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
-    __shared__ uint32_t s_tfn[kTeams][kRing][4];            // tile co0, co1, tot0, tot1
-    __shared__ uint64_t s_O[kTeams][kRing];                 // tokens before the tile
-    __shared__ uint32_t s_C[kTeams][kRing];                 // carry into the tile
-    __shared__ uint32_t s_ticket[kTeams][kRing];
-    __shared__ uint32_t s_p1cnt[kTeams][kRing];     // phase-1 arrivals per slot (kWaves per use); waves
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroups][4];   // wave functions (phase 1)
+    __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
+    __shared__ uint32_t s_tfn[kRing][4];            // tile co0, co1, tot0, tot1
+    __shared__ uint64_t s_O[kRing];                 // tokens before the tile
+    __shared__ uint32_t s_C[kRing];                 // carry into the tile
+    __shared__ uint32_t s_ticket[kRing];
+    __shared__ uint32_t s_p1cnt[kRing];     // phase-1 arrivals per slot (kWaves per use); waves
                                                     // drift across iterations, so one counter would mix them
-    __shared__ uint32_t s_rdone[kTeams];            // iterations whose tile is resolved
-    __shared__ uint32_t s_lbdone[kTeams];           // iterations whose pending tile has C, O
-    __shared__ uint32_t s_tkdone[kTeams];           // iterations whose next ticket is in s_ticket
+    __shared__ uint32_t s_rdone;            // iterations whose tile is resolved
+    __shared__ uint32_t s_lbdone;           // iterations whose pending tile has C, O
+    __shared__ uint32_t s_tkdone;           // iterations whose next ticket is in s_ticket
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t gw = uni((uint32_t)tid >> 6);          // wave of the workgroup
-    const uint32_t team = kTeams == 1 ? 0u : gw / kWaves;          // team
-    const uint32_t wave = kTeams == 1 ? gw : gw % kWaves;          // wave within the team
-    const int ttid = kTeams == 1 ? tid : tid % (kWaves * 64);      // thread within the team
+    const uint32_t wave = uni((uint32_t)tid >> 6);
     const uint64_t n = p.n;
     const uint32_t ntiles = p.ntiles;
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
-    if (ttid == 0) {
+    if (tid == 0) {
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        s_ticket[team][0] = blockIdx.x * kTeams + team;                 // timing experiment: static round-robin tiles
+        s_ticket[0] = blockIdx.x;                 // timing experiment: static round-robin tiles
 #else
-        s_ticket[team][0] = atomicAdd(p.ctl, 1u);
+        s_ticket[0] = atomicAdd(p.ctl, 1u);
 #endif
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (kTk2) s_ticket[team][1] = s_ticket[team][0] + gridDim.x * kTeams;
+        if (kTk2) s_ticket[1] = s_ticket[0] + gridDim.x;
 #else
-        if (kTk2) s_ticket[team][1] = atomicAdd(p.ctl, 1u);   // the tile after it
-        if (kTkN) s_ticket[team][kRing - 1] = atomicAdd(p.ctl, 1u);   // read in iteration 0
+        if (kTk2) s_ticket[1] = atomicAdd(p.ctl, 1u);   // the tile after it
 #endif
-        for (int r = 0; r < kRing; ++r) s_p1cnt[team][r] = 0;
-        s_rdone[team] = 0; s_lbdone[team] = 0; s_tkdone[team] = 0;
+        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
+        s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
@@ -1352,119 +1310,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         return;
     }
 #endif
-    if constexpr (kP3) {
-        static_assert(!kPf && !kTk2 && !kTkN && kTeams == 1, "three-stage pipeline: one team, no prefetch");
-        uint32_t T = uni(s_ticket[0][0]);
-        uint32_t Tp = kNone, Tpp = kNone;   // look-back in flight; emission this iteration
-        uint32_t x[kS][4], nxt[kS];
-        if (T < ntiles) load_tile(p, T, wave, lane, x, nxt);
-        TInfo ti = {}, tip = {}, tipp = {};
-        if (T < ntiles) ti = tile_info(p, T);
-        TileState spp, sp, sc;
-        uint64_t lbs[kLbWin];
-        for (uint32_t it = 0; T < ntiles || Tp < ntiles || Tpp < ntiles; ++it) {
-            const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1), ppslot = (it - 2) & (kRing - 1);
-            uint64_t stamp[7];
-            const bool stamping = kTiming && p.debug != nullptr;
-            if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
-            if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-            uint32_t tk = kNone;
-            if (tid == 64 && T < ntiles) tk = atomicAdd(p.ctl, 1u);
-            asm volatile("" ::: "memory");
-            if (T < ntiles) {
-                if (wave == 0) __builtin_amdgcn_s_setprio(3);
-                else if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-                phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[0][slot]);
-                __builtin_amdgcn_s_setprio(0);
-                uint32_t old = 0;
-                if (lane == 0)
-                    old = __hip_atomic_fetch_add(&s_p1cnt[0][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = uni(old);
-                if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                    resolve_tile(p, T, lane, s_wfn[0][slot], s_gin[0][slot], s_tfn[0][slot]);
-                    if (lane == 0) lds_release(&s_rdone[0], it + 1u);
-                }
-            }
-            if (tid == 64) {
-                s_ticket[0][slot] = tk;
-                lds_release(&s_tkdone[0], it + 1u);
-            }
-            if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
-            if (wave == 0 && Tp < ntiles && Tp > 0) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
-            uint32_t Tn = kNone;
-            if (T < ntiles) {
-                wait_ge(p, &s_tkdone[0], it + 1u);
-                Tn = uni(s_ticket[0][slot]);
-                if (Tn >= ntiles) Tn = kNone;
-            }
-            if (Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
-            if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
-            stamp[4] = stamp[3];
-            if (Tpp < ntiles) {
-                wait_ge(p, &s_lbdone[0], it);   // released at the end of the last iteration
-                if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
-                if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
-                emit_tile(p, Tpp, tipp, cs32, wave, lane, spp, s_gin[0][ppslot], uni(s_C[0][ppslot]),
-                          uni64(s_O[0][ppslot]), s_stage[gw]);
-                __builtin_amdgcn_s_setprio(0);
-            }
-            if (wave == 0) {
-                if (Tp < ntiles) {   // fold Tp's look-back: its loads flew during the emission
-                    uint32_t C = 1u, how = 0xFFFFu, spins = 0;
-                    uint64_t O = 0ull;
-                    if (Tp > 0) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
-                    wait_ge(p, &s_rdone[0], it);   // Tp was resolved in iteration it - 1
-                    const uint32_t tf0 = uni(s_tfn[0][pslot][0]), tf1 = uni(s_tfn[0][pslot][1]);
-                    const uint32_t tf2 = uni(s_tfn[0][pslot][2]), tf3 = uni(s_tfn[0][pslot][3]);
-                    if (lane == 0) {
-                        const uint64_t end = O + (C ? tf3 : tf2);
-                        if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
-                            record_error(p, 4u, Tp, 0xFFu, O, end, C);
-                            O = 0; C = 1;
-                        }
-                        s_C[0][pslot] = C;
-                        s_O[0][pslot] = O;
-                        lds_release(&s_lbdone[0], it + 1u);
-                        const uint64_t fin = O + (C ? tf3 : tf2);
-                        if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
-                        if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
-                        if (Tp == ntiles - 1) {
-                            *p.total = fin;
-                            if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
-                        }
-                        if (p.debug) {
-                            uint64_t* d = p.debug + 4ull * Tp;
-                            d[0] = O;
-                            d[1] = ((uint64_t)C << 32) | how;
-                            d[2] = ((uint64_t)tf3 << 32) | tf2;
-                            d[3] = ((uint64_t)tf1 << 32) | tf0;
-                        }
-                    }
-                }
-            }
-            if (stamping && Tpp < ntiles && lane == 0) {
-                stamp[5] = __builtin_amdgcn_s_memtime();
-                stamp[6] = stamp[5];
-                uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tpp * kWaves + wave);
-#pragma unroll
-                for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
-            }
-            spp = sp;
-            sp = sc;
-            tipp = tip;
-            tip = ti;
-            if (Tn < ntiles) ti = tile_info(p, Tn);
-            Tpp = Tp;
-            Tp = T;
-            T = Tn;
-        }
-        return;
-    }
-    uint32_t T = uni(s_ticket[team][0]);    // tile in phase 1
+    uint32_t T = uni(s_ticket[0]);    // tile in phase 1
     uint32_t Tp = kNone;              // tile waiting for emission
     uint32_t Tq = kNone;              // kTk2: the tile after T (kPf: its bytes are loaded during T's iteration)
-    if (kTk2) { Tq = uni(s_ticket[team][1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
+    if (kTk2) { Tq = uni(s_ticket[1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
     __syncthreads();
 
     uint32_t x[kS][4];      // input bytes of each sub-tile of T
@@ -1476,7 +1325,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     if (T < ntiles) ti = tile_info(p, T);
     TileState sp, sc;       // phase-1 state of Tp (pending) and of T (current)
     uint64_t lbs[kLbWin];   // wave 0: status words for the pending tile's look-back
-    uint32_t tkc = kNone;   // kTkN, claiming lane: the ticket claimed in the previous iteration
 
     for (uint32_t it = 0; T < ntiles || Tp < ntiles; ++it) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
@@ -1486,22 +1334,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
         if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
-        if (kLbe && wave == 0 && Tp < ntiles && Tp > 0) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
-        if (kTkN && ttid == 64) {
-            if (it > 0) {
-                s_ticket[team][pslot] = tkc;
-                lds_release(&s_tkdone[team], it);
-            }
-            tkc = T < ntiles ? atomicAdd(p.ctl, 1u) : kNone;
-        }
 #if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (ttid == 64 && (kTk2 ? Tq : T) < ntiles) tk = (kTk2 ? Tq : T) + gridDim.x * kTeams;
+        if (tid == 64 && (kTk2 ? Tq : T) < ntiles) tk = (kTk2 ? Tq : T) + gridDim.x;
 #else
-        if (!kTkN && ttid == 64 && (kTk2 ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (tid == 64 && (kTk2 ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
 #endif
         asm volatile("" ::: "memory");
 
@@ -1514,24 +1354,23 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // issue priority by age: the youngest waves lose the arbiter to the older ones, finish
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
-            if (kLead && wave == 0) __builtin_amdgcn_s_setprio(3);
-            else if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[team][slot]);
+            if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
-                old = __hip_atomic_fetch_add(&s_p1cnt[team][slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
-            lbw = (kLbe || kLead) ? wave == 0 : old == (uint32_t)kWaves * (it / kRing);
+            lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile(p, T, lane, s_wfn[team][slot], s_gin[team][slot], s_tfn[team][slot]);
-                if (lane == 0) lds_release(&s_rdone[team], it + 1u);
+                resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                if (lane == 0) lds_release(&s_rdone, it + 1u);
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        if (!kTkN && !kTk2 && ttid == 64) {
-            s_ticket[team][slot] = tk;
-            lds_release(&s_tkdone[team], it + 1u);
+        if (!kTk2 && tid == 64) {
+            s_ticket[slot] = tk;
+            lds_release(&s_tkdone, it + 1u);
         }
         if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
@@ -1541,12 +1380,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
-            if (lb && !kLbe) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
-            wait_ge(p, &s_rdone[team], it);
-            const uint32_t tf0 = uni(s_tfn[team][pslot][0]), tf1 = uni(s_tfn[team][pslot][1]);
-            const uint32_t tf2 = uni(s_tfn[team][pslot][2]), tf3 = uni(s_tfn[team][pslot][3]);
+            wait_ge(p, &s_rdone, it);
+            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, kTiming ? &bad : nullptr);
             if (lane == 0) {
                 const uint64_t end = O + (C ? tf3 : tf2);
@@ -1555,9 +1394,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     O = 0; C = 1;
                 }
                 // the other waves need only C and O: release them first, publish after
-                s_C[team][pslot] = C;
-                s_O[team][pslot] = O;
-                lds_release(&s_lbdone[team], it + 1u);
+                s_C[pslot] = C;
+                s_O[pslot] = O;
+                lds_release(&s_lbdone, it + 1u);
                 const uint64_t fin = O + (C ? tf3 : tf2);
                 if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
@@ -1584,22 +1423,22 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // T's bytes are consumed: the loads fly during the emission
         uint32_t Tn = kNone;
         if (!kTk2 && T < ntiles) {
-            wait_ge(p, &s_tkdone[team], kTkN ? it : it + 1u);
-            Tn = uni(s_ticket[team][kTkN ? pslot : slot]);
+            wait_ge(p, &s_tkdone, it + 1u);
+            Tn = uni(s_ticket[slot]);
             if (Tn >= ntiles) Tn = kNone;
         }
         if (kTk2 && !kPf) Tn = Tq;
         if (!kPf && Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
         if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
-            wait_ge(p, &s_lbdone[team], it + 1u);
+            wait_ge(p, &s_lbdone, it + 1u);
             if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
 #if defined(BLT_EXP) && (BLT_EXP & 8)
             if (Tp == kNone - 1u)   // timing experiment: no emission
 #endif
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
-            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[team][pslot], uni(s_C[team][pslot]), uni64(s_O[team][pslot]),
-                      s_stage[gw]);
+            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], uni(s_C[pslot]), uni64(s_O[pslot]),
+                      s_stage[wave]);
             __builtin_amdgcn_s_setprio(0);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
@@ -1609,21 +1448,21 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #pragma unroll
             for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
         }
-        if (stamping && ttid == 0 && Tp < ntiles) {
+        if (stamping && tid == 0 && Tp < ntiles) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
             e[2] = __builtin_amdgcn_s_memtime();
         }
         if (kTk2) {
             // Tq <- the ticket claimed at this iteration's start (handed over after the claiming
             // wave's emission: a whole iteration for the atomic); kPf: T <- Tq's bytes, loaded then
-            if (ttid == 64) {
-                s_ticket[team][slot] = tk;
-                lds_release(&s_tkdone[team], it + 1u);
+            if (tid == 64) {
+                s_ticket[slot] = tk;
+                lds_release(&s_tkdone, it + 1u);
             }
             uint32_t Tr = kNone;
             if (Tq < ntiles) {
-                wait_ge(p, &s_tkdone[team], it + 1u);
-                Tr = uni(s_ticket[team][slot]);
+                wait_ge(p, &s_tkdone, it + 1u);
+                Tr = uni(s_ticket[slot]);
                 if (Tr >= ntiles) Tr = kNone;
                 if (kPf) {
 #pragma unroll
