@@ -564,9 +564,10 @@ constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
 // Per-wave token stage: a wave range of 1024 positions emits 512..1024 tokens; the stage holds
-// 521 (2-byte aligned start + up to 1042 bytes).  A range with more tokens goes through it in two
-// parts of 32 lanes (at most 512 tokens each).
-constexpr int kStageWave = 1056;
+// 761 (2-byte aligned start + up to 1522 bytes), all the LDS the table leaves: every range of text
+// or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
+// in two parts of 32 lanes (at most 512 tokens each).
+constexpr int kStageWave = 1536;
 #ifdef BLT_LBWIN
 constexpr int kLbWin = BLT_LBWIN;                      // look-back windows of 64 per round trip
 #else

@@ -1,7 +1,7 @@
 """Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook, in
 the timing build build/exp/libblt_bpe_timing.so from `make exp`, or BLT_LIB_PATH).
 
-    python tools/tile_timing.py [MiB]
+    python tools/tile_timing.py [MiB] [--random]     (--random: cfg5's random bytes instead of cfg3's text)
 Prints mean/median cycles of phase 1 (lookups + wave functions), phase 2 (tile resolve +
 look-back), phase 3 (emission + copy-out) and the look-back window statistics."""
 import ctypes
@@ -24,11 +24,13 @@ CHUNK = 16 << 20
 
 
 def main():
-    mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    mib = int(args[0]) if args else 1024
     n = mib << 20
     merges = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
     s = blt_amd.BpeStrategy(merges)
-    d_in = torch.from_numpy(synth.text(n, seed=3)).cuda()
+    data = synth.random_bytes(n, seed=5) if "--random" in sys.argv else synth.text(n, seed=3)   # cfg5 / cfg3
+    d_in = torch.from_numpy(data).cuda()
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     wsb = s.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")

@@ -12,6 +12,8 @@ for v in "$@"; do
   case $v in
     *:t) n=${v%:t}; BLT_LIB_PATH=$R/build/exp/libblt_bpe_$n.so timeout -k 10 200 python tools/tile_timing.py > "$O/timing_$n.txt" 2>&1
          head -18 "$O/timing_$n.txt"; continue;;
+    *:tr) n=${v%:tr}; BLT_LIB_PATH=$R/build/exp/libblt_bpe_$n.so timeout -k 10 200 python tools/tile_timing.py --random > "$O/timing_r_$n.txt" 2>&1
+         head -18 "$O/timing_r_$n.txt"; continue;;
   esac
   notest=0
   case $v in *:b) v=${v%:b}; notest=1;; esac   # NAME:b = bench only (timing experiments with wrong output)
