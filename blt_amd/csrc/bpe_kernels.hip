@@ -1487,27 +1487,58 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 
 }  // namespace seg
 
-// Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).
+// Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).  A streaming copy
+// that doubles the bytes: each thread takes kBasicVec 16-byte input blocks a block-stride apart
+// (all loads issued before any store) and writes each as two 16-byte output blocks.
+#ifndef BLT_BASIC_VEC
+#define BLT_BASIC_VEC 4
+#endif
+#ifndef BLT_BASIC_NT
+#define BLT_BASIC_NT 0
+#endif
+#ifndef BLT_BASIC_BLOCKS
+#define BLT_BASIC_BLOCKS 65536
+#endif
+constexpr int kBasicVec = BLT_BASIC_VEC;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+template <typename T> __device__ __forceinline__ T ld_stream(const T* p) {
+    if constexpr ((BLT_BASIC_NT & 1) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename T> __device__ __forceinline__ void st_stream(T v, T* p) {
+    if constexpr ((BLT_BASIC_NT & 2) != 0) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void basic_expand16(v4u w, v4u* dst) {
+    v4u a, b;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        a[2 * q] = __builtin_amdgcn_perm(w[q], 0u, 0x050C040Cu);           // [0, b0, 0, b1]
+        a[2 * q + 1] = __builtin_amdgcn_perm(w[q], 0u, 0x070C060Cu);       // [0, b2, 0, b3]
+        b[2 * q] = __builtin_amdgcn_perm(w[q + 2], 0u, 0x050C040Cu);
+        b[2 * q + 1] = __builtin_amdgcn_perm(w[q + 2], 0u, 0x070C060Cu);
+    }
+    st_stream(a, dst);
+    st_stream(b, dst + 1);
+}
 __global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                            uint8_t* __restrict__ out) {
     const uint64_t nvec = n / 16;
+    const v4u* src = reinterpret_cast<const v4u*>(in);
+    v4u* dst = reinterpret_cast<v4u*>(out);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-        uint4 v = reinterpret_cast<const uint4*>(in)[i];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint32_t o[8];
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (kBasicVec - 1) * stride < nvec; i += kBasicVec * stride) {
+        v4u v[kBasicVec];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            o[2 * q] = ((w[q] & 0xFFu) << 8) | ((w[q] & 0xFF00u) << 16);
-            o[2 * q + 1] = ((w[q] >> 8) & 0xFF00u) | (w[q] & 0xFF000000u);
-        }
-        uint4* dst = reinterpret_cast<uint4*>(out) + 2 * i;
-        dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-        dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        for (int u = 0; u < kBasicVec; ++u) v[u] = ld_stream(src + i + u * stride);
+#pragma unroll
+        for (int u = 0; u < kBasicVec; ++u) basic_expand16(v[u], dst + 2 * (i + u * stride));
     }
-    for (uint64_t i = nvec * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        out[2 * i] = 0;
-        out[2 * i + 1] = in[i];
+    for (; i < nvec; i += stride) basic_expand16(src[i], dst + 2 * i);
+    for (uint64_t k = nvec * 16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+        out[2 * k] = 0;
+        out[2 * k + 1] = in[k];
     }
 }
 
@@ -1587,9 +1618,9 @@ hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, 
 
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    uint64_t blocks = (n / 16 + 255) / 256;
+    uint64_t blocks = (n / 16 / kBasicVec + 255) / 256;   // one pass of kBasicVec blocks per thread
     if (blocks < 1) blocks = 1;
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > BLT_BASIC_BLOCKS) blocks = BLT_BASIC_BLOCKS;
     hipLaunchKernelGGL(basic_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
     return hipGetLastError();
 }
