@@ -1099,18 +1099,25 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             const uint32_t hend = ((rgp + 15u) & ~15u) < re ? ((rgp + 15u) & ~15u) : re;
             const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
             const uint32_t nfull = (tbeg - hend) >> 4;
+            // at most 95 whole blocks (1522 bytes): two per lane; all LDS reads issued before the
+            // one wait, so the stage's read latency is paid once
+            static_assert(kStageWave <= 2 * 64 * 16, "copy-out: at most two blocks per lane");
+            const uint32_t o0 = hend + 16u * (uint32_t)lane, o1 = o0 + 1024u;
+            const bool b0 = (uint32_t)lane < nfull, b1 = (uint32_t)lane + 64u < nfull;
+            const uint32_t of = lane < 8 ? rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+            const bool bf = lane < 16 && of < (lane < 8 ? hend : re);
+            u32x4 v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
+            uint16_t vf = 0;
+            if (b0) v0 = *reinterpret_cast<const u32x4*>(stg + o0);
+            if (b1) v1 = *reinterpret_cast<const u32x4*>(stg + o1);
+            if (bf) vf = st16[of >> 1];
 #if defined(BLT_EXP) && (BLT_EXP & 4)
             if (nfull == 12345u)   // timing experiment: no copy-out
 #endif
-            for (uint32_t i = (uint32_t)lane; i < nfull; i += 64) {
-                const uint32_t o = hend + 16u * i;
-                const u32x4 v = *reinterpret_cast<const u32x4*>(stg + o);
-                __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)(abp + o), 0, 0);
-            }
-            if (lane < 16) {
-                const uint32_t o = lane < 8 ? rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
-                const uint32_t lim = lane < 8 ? hend : re;
-                if (o < lim) __builtin_amdgcn_raw_buffer_store_b16(st16[o >> 1], ro, (int)(abp + o), 0, 0);
+            {
+                if (b0) __builtin_amdgcn_raw_buffer_store_b128(v0, ro, (int)(abp + o0), 0, 0);
+                if (b1) __builtin_amdgcn_raw_buffer_store_b128(v1, ro, (int)(abp + o1), 0, 0);
+                if (bf) __builtin_amdgcn_raw_buffer_store_b16(vf, ro, (int)(abp + of), 0, 0);
             }
         }
     }
