@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -362,10 +363,7 @@ int read_u64(const void* dptr, uint64_t* v, hipStream_t s) {
     return 0;
 }
 
-int check_ctl(uint8_t* ws, hipStream_t s) {
-    uint32_t ctl[16] = {0};
-    HIP_TRY(hipMemcpyAsync(ctl, ws, sizeof ctl, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+int ctl_error(const uint32_t* ctl) {
     if (ctl[1])
         return fail(BLT_E_IO,
                     "merge-scan device check failed (flags 0x%x: 1 look-back timeout, 2 output range, 4 prefix "
@@ -373,6 +371,13 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
                     ctl[1], ctl[2] ? ctl[2] - 1 : 0, ctl[3], (unsigned long long)ctl[4] | ((unsigned long long)ctl[5] << 32),
                     (unsigned long long)ctl[6] | ((unsigned long long)ctl[7] << 32), ctl[8]);
     return 0;
+}
+
+int check_ctl(uint8_t* ws, hipStream_t s) {
+    uint32_t ctl[16] = {0};
+    HIP_TRY(hipMemcpyAsync(ctl, ws, sizeof ctl, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return ctl_error(ctl);
 }
 
 // Enqueues one merge pass over n positions.
@@ -472,8 +477,30 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
 }
 
 // ---- per-device staging contexts for the host-buffer API ---------------------------------
+// One slot of the pipelined host path: device buffers for a window of whole chunks, its own
+// stream, a pinned record of the window's token count, control words and chunk offsets.
+struct PipeSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t counted = nullptr;     // the window's kernel and record copy are done
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    uint8_t* d_ws = nullptr;
+    uint64_t* d_off = nullptr;
+    uint64_t* h_rec = nullptr;        // pinned: [0] tokens, [1..8] control words, [9..] chunk offsets
+    uint64_t win = 0, ws_bytes = 0, nch = 0;
+};
+#ifndef BLT_PIPE_SLOTS
+#define BLT_PIPE_SLOTS 4
+#endif
+#ifndef BLT_PIPE_WIN_MIB
+#define BLT_PIPE_WIN_MIB 32
+#endif
+constexpr int kPipeSlots = BLT_PIPE_SLOTS;
+constexpr uint64_t kPipeWindow = (uint64_t)BLT_PIPE_WIN_MIB << 20;   // bytes per window, whole chunks
+
 struct DevCtx {
     int device = 0;
+    PipeSlot pipe[kPipeSlots];
     hipStream_t stream = nullptr;
     uint8_t* d_in = nullptr;
     size_t in_cap = 0;
@@ -530,12 +557,17 @@ struct CtxGuard {
 
 // Encodes host bytes [in, in + n) (chunk size cs) on device dev into host out; returns
 // tokens and optional per-chunk token offsets (nchunks + 1).
+int encode_host_pipelined(const blt_bpe* h, DevCtx* c, const uint8_t* in, uint64_t n, uint64_t cs, uint8_t* out,
+                          uint64_t* tokens, std::vector<uint64_t>* chunk_off);
+
 int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uint64_t cs, uint8_t* out,
                    uint64_t* tokens, std::vector<uint64_t>* chunk_off) {
     HIP_TRY(hipSetDevice(dev));
     DevCtx* c = ctx_acquire(dev);
     if (!c) return fail(BLT_E_IO, "cannot create a HIP stream on device %d", dev);
     CtxGuard guard{c};
+    if (h->single_pass && n > kPipeWindow && cs <= kPipeWindow / 2)
+        return encode_host_pipelined(h, c, in, n, cs, out, tokens, chunk_off);
     const WsLayout L = ws_layout(h->single_pass, n, cs);
     if (int rc = grow(&c->d_in, &c->in_cap, up16(n))) return rc;
     if (int rc = grow(&c->d_out, &c->out_cap, up16(2 * n))) return rc;
@@ -553,6 +585,132 @@ int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uin
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     *tokens = ntok;
+    return 0;
+}
+
+// Grows slot P of c for windows of `win` bytes in chunks of cs (device buffers, stream, event,
+// pinned record).  Slots are cached with the context for the process lifetime.
+int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs) {
+    const uint64_t nch = (win + cs - 1) / cs;
+    const WsLayout L = ws_layout(h->single_pass, win, cs);
+    if (!P.stream) HIP_TRY(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
+    if (!P.counted) HIP_TRY(hipEventCreateWithFlags(&P.counted, hipEventDisableTiming));
+    if (P.win < win || P.ws_bytes < L.bytes || P.nch < nch) {
+        if (P.d_in) (void)hipFree(P.d_in);
+        if (P.d_out) (void)hipFree(P.d_out);
+        if (P.d_ws) (void)hipFree(P.d_ws);
+        if (P.d_off) (void)hipFree(P.d_off);
+        if (P.h_rec) (void)hipHostFree(P.h_rec);
+        P.d_in = P.d_out = P.d_ws = nullptr;
+        P.d_off = P.h_rec = nullptr;
+        P.win = P.ws_bytes = P.nch = 0;
+        HIP_TRY(hipMalloc(&P.d_in, up16(win)));
+        HIP_TRY(hipMalloc(&P.d_out, up16(2 * win)));
+        HIP_TRY(hipMalloc(&P.d_ws, L.bytes));
+        HIP_TRY(hipMalloc(&P.d_off, 8 * (nch + 1)));
+        HIP_TRY(hipHostMalloc(&P.h_rec, 8 * (9 + nch + 1), hipHostMallocDefault));
+        P.win = win;
+        P.ws_bytes = L.bytes;
+        P.nch = nch;
+    }
+    return 0;
+}
+
+// The host-buffer path for single-pass maps, pipelined over windows of whole chunks (chunks are
+// independent, pipeline.rs:73-81): one thread copies window w to the device and launches its
+// merge scan while a second thread copies window w - 1's tokens back to the host behind the
+// last one, in chunk order (pipeline.rs:153-192).  H2D and D2H run at the same time, on the
+// two DMA directions; each window's output lands at its final place in `out`.
+int encode_host_pipelined(const blt_bpe* h, DevCtx* c, const uint8_t* in, uint64_t n, uint64_t cs, uint8_t* out,
+                          uint64_t* tokens, std::vector<uint64_t>* chunk_off) {
+    const uint64_t win = std::max<uint64_t>(cs, kPipeWindow / cs * cs);
+    const uint64_t nw = (n + win - 1) / win;
+    for (int k = 0; k < kPipeSlots; ++k)
+        if (int rc = pipe_slot_ready(h, c->pipe[k], std::min(win, n), cs)) return rc;
+    if (chunk_off) chunk_off->assign(1, 0);
+
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t launched = 0;     // windows whose kernel and record copy are enqueued
+    uint64_t drained = 0;      // windows whose D2H is enqueued (their slot may be reused)
+    int rc_prod = 0, rc_cons = 0;
+    std::string err_prod, err_cons;
+    const int dev = c->device;
+
+    std::thread producer([&] {
+        int rc = hipSetDevice(dev) == hipSuccess ? 0 : fail(BLT_E_IO, "hipSetDevice(%d) failed", dev);
+        for (uint64_t w = 0; w < nw && !rc; ++w) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return rc_cons || drained + kPipeSlots > w; });
+                if (rc_cons) break;
+            }
+            PipeSlot& P = c->pipe[w % kPipeSlots];
+            const uint64_t b0 = w * win, len = std::min(win, n - b0);
+            const WsLayout L = ws_layout(true, len, cs);
+            if (hipMemcpyAsync(P.d_in, in + b0, len, hipMemcpyHostToDevice, P.stream) != hipSuccess) {
+                rc = fail(BLT_E_IO, "host-to-device copy failed");
+                break;
+            }
+            if ((rc = encode_device(h, P.d_in, len, cs, P.d_out, P.d_off, P.d_ws, P.ws_bytes, P.stream, nullptr))) break;
+            if (hipMemcpyAsync(P.h_rec, P.d_ws + L.total, 8, hipMemcpyDeviceToHost, P.stream) != hipSuccess ||
+                hipMemcpyAsync(P.h_rec + 1, P.d_ws + L.ctl, 64, hipMemcpyDeviceToHost, P.stream) != hipSuccess ||
+                hipMemcpyAsync(P.h_rec + 9, P.d_off, 8 * (L.nchunks + 1), hipMemcpyDeviceToHost, P.stream) != hipSuccess ||
+                hipEventRecord(P.counted, P.stream) != hipSuccess) {
+                rc = fail(BLT_E_IO, "record copy failed");
+                break;
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            ++launched;
+            cv.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        if (rc) { rc_prod = rc; err_prod = t_err; }
+        cv.notify_all();
+    });
+
+    uint64_t pos = 0;   // tokens written so far
+    int rc = 0;
+    for (uint64_t w = 0; w < nw; ++w) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return rc_prod || launched > w; });
+            if (launched <= w) break;   // the producer failed before launching w
+        }
+        PipeSlot& P = c->pipe[w % kPipeSlots];
+        const uint64_t len = std::min(win, n - w * win);
+        const uint64_t nch = (len + cs - 1) / cs;
+        if (hipEventSynchronize(P.counted) != hipSuccess) { rc = fail(BLT_E_IO, "merge scan failed on device %d", dev); break; }
+        uint32_t ctl[16];
+        memcpy(ctl, P.h_rec + 1, sizeof ctl);
+        if ((rc = ctl_error(ctl))) break;
+        const uint64_t tok = P.h_rec[0];
+        if (chunk_off) {
+            for (uint64_t k = 1; k <= nch; ++k) chunk_off->push_back(pos + P.h_rec[9 + k]);
+        }
+        if (hipMemcpyAsync(out + 2 * pos, P.d_out, 2 * tok, hipMemcpyDeviceToHost, P.stream) != hipSuccess) {
+            rc = fail(BLT_E_IO, "device-to-host copy failed");
+            break;
+        }
+        pos += tok;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            ++drained;
+            cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (rc) rc_cons = rc;
+        cv.notify_all();
+    }
+    producer.join();
+    for (int k = 0; k < kPipeSlots; ++k)
+        if (c->pipe[k].stream && hipStreamSynchronize(c->pipe[k].stream) != hipSuccess && !rc)
+            rc = fail(BLT_E_IO, "device-to-host copy failed");
+    if (rc_prod && !rc) return fail(rc_prod, "%s", err_prod.c_str());
+    if (rc) return rc;
+    *tokens = pos;
     return 0;
 }
 

@@ -272,3 +272,16 @@ def test_dense_wave_ranges(cs):
     exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
     assert np.array_equal(got, exp)
     assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("cs,n", [(16 << 20, (200 << 20) + 12345), (1 << 20, (130 << 20) + 1), (300001, 70 << 20)])
+def test_host_path_pipelined_windows(cs, n):
+    """Host buffers over several 64 MiB windows (the pipelined blt_bpe_process_chunks path):
+    stitched output and per-chunk lengths bit-exact, last window partial."""
+    text = synth.text(n, seed=7)
+    m = synth.merges_dict(synth.top_pair_merges(text[: 8 << 20], 256))
+    s = blt_amd.BpeStrategy(m)
+    got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(text, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)

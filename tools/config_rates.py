@@ -12,6 +12,7 @@ Rows (inputs resident in HBM, kernel time from HIP events on the launch stream, 
   host   cfg3 through blt_bpe_process_chunks from pageable host memory (PCIe-inclusive)
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -109,14 +110,29 @@ def main():
         res["multi"] = row(tm.size, ms, tok, bool(np.array_equal(got, O.COracle(mm).run(tm, CHUNK, threads=16))),
                            passes="general map (chained and byte-valued merges)")
     if "host" in only:
+        # blt_bpe_process_chunks from pageable host memory into a caller buffer: the first call pays
+        # device allocations and first-touch page faults of the output; steady state reuses both
         t3 = synth.text(n, seed=3)
-        s3.process_chunks(t3[:1 << 20], CHUNK)
+        lib, h = blt_amd._lib.lib(), s3.handle
+        out = np.empty(2 * n, np.uint8)
+        olen = ctypes.c_size_t(0)
+
+        def call():
+            blt_amd._lib.check(lib.blt_bpe_process_chunks(h, t3.ctypes.data, n, CHUNK, 1, out.ctypes.data, out.size,
+                                                          ctypes.byref(olen), None))
         t0 = time.perf_counter()
-        out = s3.process_chunks(t3, CHUNK)
-        dt = time.perf_counter() - t0
+        call()
+        cold = time.perf_counter() - t0
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        dt = float(np.median(ts))
         exp = O.COracle(m3).run(t3, CHUNK, threads=16)
         res["host"] = {"bytes": n, "seconds": round(dt, 4), "input_GBps": round(n / dt / 1e9, 3),
-                       "bit_exact": bool(np.array_equal(out, exp))}
+                       "cold_seconds": round(cold, 4),
+                       "bit_exact": bool(np.array_equal(out[:olen.value], exp))}
     print(json.dumps(res, indent=1))
 
 
