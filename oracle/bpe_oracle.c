@@ -376,6 +376,79 @@ size_t oracle_run_chunks(const omap *m, int passthrough, const uint8_t *in, size
 }
 
 // ---------------------------------------------------------------------------------------
+// "Optimised CPU" line of SURVEY.md §8(d), timed beside the faithful restatement above for
+// fairness: the same greedy scan (tokenizer.rs:63-81) for a single-pass byte-pair map (no map
+// value is a key component, so one pass is the fixpoint), over a dense 64K-entry table instead
+// of a hash map, one pass per chunk, big-endian writes, chunks over pthreads.  Table entry
+// (a << 8 | b) = value + 1, or 0 for no merge.  Baseline only: never a checker.
+// ---------------------------------------------------------------------------------------
+typedef struct {
+    const uint32_t *tab; const uint8_t *in; size_t n; size_t cs; size_t nchunks;
+    uint8_t *scratch; size_t *lens; size_t next; pthread_mutex_t mu;
+} fast_ctx;
+
+static size_t fast_chunk(const uint32_t *tab, const uint8_t *in, size_t n, uint8_t *out) {
+    size_t o = 0, i = 0;
+    while (i + 1 < n) {   // branch-free: the merge outcome only moves i
+        const uint32_t v = tab[((uint32_t)in[i] << 8) | in[i + 1]];
+        const uint32_t t = v ? v - 1 : in[i];
+        out[o] = (uint8_t)(t >> 8);
+        out[o + 1] = (uint8_t)t;
+        o += 2;
+        i += 1 + (v != 0);
+    }
+    if (i < n) { out[o] = 0; out[o + 1] = in[i]; o += 2; }
+    return o;
+}
+
+static void *fast_worker(void *arg) {
+    fast_ctx *c = (fast_ctx *)arg;
+    for (;;) {
+        pthread_mutex_lock(&c->mu);
+        size_t k = c->next++;
+        pthread_mutex_unlock(&c->mu);
+        if (k >= c->nchunks) break;
+        size_t st = k * c->cs, len = c->n - st < c->cs ? c->n - st : c->cs;
+        c->lens[k] = fast_chunk(c->tab, c->in + st, len, c->scratch + 2 * st);
+    }
+    return NULL;
+}
+
+// Returns the output bytes, or (size_t)-1 when the map is not a single-pass byte-pair map.
+size_t oracle_fast_run_chunks(const uint16_t *a, const uint16_t *b, const uint16_t *v, size_t nm, const uint8_t *in,
+                              size_t n, size_t chunk_size, int threads, uint8_t *out) {
+    uint32_t *tab = (uint32_t *)calloc(65536, sizeof(uint32_t));
+    uint8_t *comp = (uint8_t *)calloc(65536, 1);
+    for (size_t i = 0; i < nm; ++i) {
+        if (a[i] > 255 || b[i] > 255) { free(tab); free(comp); return (size_t)-1; }
+        tab[((uint32_t)a[i] << 8) | b[i]] = (uint32_t)v[i] + 1;   // a later duplicate overwrites
+        comp[a[i]] = comp[b[i]] = 1;
+    }
+    for (size_t i = 0; i < nm; ++i)
+        if (comp[v[i]]) { free(tab); free(comp); return (size_t)-1; }
+    free(comp);
+    if (n == 0) { free(tab); return 0; }
+    fast_ctx c;
+    memset(&c, 0, sizeof c);
+    c.tab = tab; c.in = in; c.n = n; c.cs = chunk_size;
+    c.nchunks = (n + chunk_size - 1) / chunk_size;
+    c.scratch = (uint8_t *)malloc(2 * n);
+    c.lens = (size_t *)calloc(c.nchunks, sizeof(size_t));
+    pthread_mutex_init(&c.mu, NULL);
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > c.nchunks) threads = (int)c.nchunks;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    for (int t = 1; t < threads; ++t) pthread_create(&th[t], NULL, fast_worker, &c);
+    fast_worker(&c);
+    for (int t = 1; t < threads; ++t) pthread_join(th[t], NULL);
+    size_t o = 0;
+    for (size_t k = 0; k < c.nchunks; ++k) { memcpy(out + o, c.scratch + 2 * k * chunk_size, c.lens[k]); o += c.lens[k]; }
+    pthread_mutex_destroy(&c.mu);
+    free(th); free(c.lens); free(c.scratch); free(tab);
+    return o;
+}
+
+// ---------------------------------------------------------------------------------------
 // parse_chunk_size_str — blt_core/src/utils.rs:10-45.  KB/MB are 1024-based, raw digits are
 // bytes; the multiply wraps (release build).  Returns 0 ok, 1 error (msg = reference text).
 // ---------------------------------------------------------------------------------------

@@ -259,6 +259,9 @@ def _load():
     lib.oracle_run_chunks.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                       ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_void_p]
+    lib.oracle_fast_run_chunks.restype = ctypes.c_size_t
+    lib.oracle_fast_run_chunks.argtypes = [u16p, u16p, u16p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     lib.oracle_load_merges.restype = ctypes.c_int
     lib.oracle_load_merges.argtypes = [ctypes.c_char_p, u16p, u16p, u16p, ctypes.c_size_t,
                                        ctypes.POINTER(ctypes.c_size_t), ctypes.c_char_p, ctypes.c_size_t]
@@ -328,6 +331,26 @@ class COracle:
         if return_lens:
             return res, lens[:nchunks].astype(np.int64)
         return res
+
+
+def fast_run(merges: Dict[Tuple[int, int], int], data, chunk_size: int, threads: int = 1):
+    """The "optimised CPU" line: dense table, one greedy pass per chunk, for a
+    single-pass byte-pair map.  A baseline for bench.py, never a checker.  Returns None for maps
+    it does not cover (u16 keys, or a value that is a key component)."""
+    import numpy as np
+    lib = _load()
+    items = list(merges.items())
+    nm = len(items)
+    A = (ctypes.c_uint16 * max(nm, 1))(*[k[0] for k, _ in items])
+    B = (ctypes.c_uint16 * max(nm, 1))(*[k[1] for k, _ in items])
+    V = (ctypes.c_uint16 * max(nm, 1))(*[v for _, v in items])
+    ptr, keep = _as_buffer(data)
+    n = len(data)
+    out = np.empty(max(2 * n, 1), dtype=np.uint8)
+    m = lib.oracle_fast_run_chunks(A, B, V, nm, ptr, n, chunk_size, threads, out.ctypes.data)
+    if m == ctypes.c_size_t(-1).value:
+        return None
+    return out[:m]
 
 
 def c_load_merges(path: str) -> Dict[Tuple[int, int], int]:

@@ -108,3 +108,17 @@ def test_cli_kats_through_pipeline(kats):
             exp += c["content_token"].to_bytes(2, "big")
         exp += data if c["mode"] == "passthrough" else O.basic_process_chunk(data)
         assert got == bytes(exp), c["name"]
+
+
+def test_optimized_cpu_line_matches_restatement():
+    """bench.py's "optimised CPU" baseline (dense table, one pass) equals the faithful C
+    restatement on single-pass byte-pair maps and declines the maps it does not cover."""
+    import numpy as np
+    from blt_amd import synth
+    from oracle import oracle as O
+    text = synth.text(3 << 20, seed=9)
+    m = synth.merges_dict(synth.text_merges_50k(text[: 1 << 20], seed=9))
+    for cs in (4096, 300001, 1 << 20):
+        assert np.array_equal(O.fast_run(m, text, cs, threads=4), O.COracle(m).run(text, cs, threads=4))
+    assert O.fast_run({(97, 98): 256, (256, 99): 257}, text[:100], 64) is None   # u16 key
+    assert O.fast_run({(97, 98): 99, (99, 99): 300}, text[:100], 64) is None     # value is a key component
