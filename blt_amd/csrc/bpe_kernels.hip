@@ -557,9 +557,17 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
     asm("v_lshl_add_u32 %0, %1, 1, %0" : "+v"(a) : "v"(bit));
 }
 
-constexpr int kThreads = 1024;                         // 16 waves: 4 per SIMD hide LDS and VALU latency
+// Workgroup geometry: BLT_WAVES waves (16: 4 per SIMD, 128 VGPRs each; 8: 2 per SIMD, 256 VGPRs
+// each) times BLT_KS sub-tiles per wave make one 32 KiB tile.
+#ifndef BLT_WAVES
+#define BLT_WAVES 16
+#endif
+#ifndef BLT_KS
+#define BLT_KS (32 / BLT_WAVES)
+#endif
+constexpr int kThreads = 64 * BLT_WAVES;
 constexpr int kWaves = kThreads / 64;
-constexpr int kS = 2;                                  // sub-tiles per tile
+constexpr int kS = BLT_KS;                             // sub-tiles per tile
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
@@ -567,7 +575,7 @@ constexpr int kGroups = kS * kWaves;
 // 761 (2-byte aligned start + up to 1522 bytes), all the LDS the table leaves: every range of text
 // or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
 // in two parts of 32 lanes (at most 512 tokens each).
-constexpr int kStageWave = 1536;
+constexpr int kStageWave = 1536 * (16 / kWaves);    // the LDS the table leaves, shared by the waves
 #ifdef BLT_LBWIN
 constexpr int kLbWin = BLT_LBWIN;                      // look-back windows of 64 per round trip
 #else
@@ -1099,24 +1107,27 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             const uint32_t hend = ((rgp + 15u) & ~15u) < re ? ((rgp + 15u) & ~15u) : re;
             const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
             const uint32_t nfull = (tbeg - hend) >> 4;
-            // at most 95 whole blocks (1522 bytes): two per lane; all LDS reads issued before the
-            // one wait, so the stage's read latency is paid once
-            static_assert(kStageWave <= 2 * 64 * 16, "copy-out: at most two blocks per lane");
-            const uint32_t o0 = hend + 16u * (uint32_t)lane, o1 = o0 + 1024u;
-            const bool b0 = (uint32_t)lane < nfull, b1 = (uint32_t)lane + 64u < nfull;
+            // whole blocks: at most kCopyBlk per lane; all LDS reads issued before the one wait, so
+            // the stage's read latency is paid once
+            constexpr int kCopyBlk = (kStageWave + 1023) / 1024;
+            u32x4 vb[kCopyBlk];
             const uint32_t of = lane < 8 ? rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
             const bool bf = lane < 16 && of < (lane < 8 ? hend : re);
-            u32x4 v0 = {0u, 0u, 0u, 0u}, v1 = {0u, 0u, 0u, 0u};
             uint16_t vf = 0;
-            if (b0) v0 = *reinterpret_cast<const u32x4*>(stg + o0);
-            if (b1) v1 = *reinterpret_cast<const u32x4*>(stg + o1);
+#pragma unroll
+            for (int q = 0; q < kCopyBlk; ++q) {
+                vb[q] = (u32x4){0u, 0u, 0u, 0u};
+                if ((uint32_t)lane + 64u * q < nfull) vb[q] = *reinterpret_cast<const u32x4*>(stg + hend + 16u * lane + 1024u * q);
+            }
             if (bf) vf = st16[of >> 1];
 #if defined(BLT_EXP) && (BLT_EXP & 4)
             if (nfull == 12345u)   // timing experiment: no copy-out
 #endif
             {
-                if (b0) __builtin_amdgcn_raw_buffer_store_b128(v0, ro, (int)(abp + o0), 0, 0);
-                if (b1) __builtin_amdgcn_raw_buffer_store_b128(v1, ro, (int)(abp + o1), 0, 0);
+#pragma unroll
+                for (int q = 0; q < kCopyBlk; ++q)
+                    if ((uint32_t)lane + 64u * q < nfull)
+                        __builtin_amdgcn_raw_buffer_store_b128(vb[q], ro, (int)(abp + hend + 16u * lane + 1024u * q), 0, 0);
                 if (bf) __builtin_amdgcn_raw_buffer_store_b16(vf, ro, (int)(abp + of), 0, 0);
             }
         }
