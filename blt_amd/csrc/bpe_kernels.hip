@@ -1315,14 +1315,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #else
             if (Tb < ntiles) load_tile(p, Tb, wave, lane, xb, nb);
 #endif
-            phase1_tile<kBE, kHiM>(tab, xa, na, tile_info(p, Ta), cs32, wave, lane, st, s_wfn[0][(it++) & 3]);
+            phase1_tile<kBE, kHiM>(tab, xa, na, tile_info(p, Ta), cs32, wave, lane, st, s_wfn[(it++) & 3]);
             acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
             if (Tb >= ntiles) break;
             const uint32_t Tc = Tb + gridDim.x;
 #if !(BLT_EXP & 8192)
             if (Tc < ntiles) load_tile(p, Tc, wave, lane, xa, na);
 #endif
-            phase1_tile<kBE, kHiM>(tab, xb, nb, tile_info(p, Tb), cs32, wave, lane, st, s_wfn[0][(it++) & 3]);
+            phase1_tile<kBE, kHiM>(tab, xb, nb, tile_info(p, Tb), cs32, wave, lane, st, s_wfn[(it++) & 3]);
             acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
         }
         if (acc == 0x9E3779B9u) p.ctl[15] = acc;
