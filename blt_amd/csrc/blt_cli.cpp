@@ -34,9 +34,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -178,16 +180,52 @@ std::string lib_error(int rc) {
 // Ordered sink over a file descriptor; write_all retries short writes.
 struct Sink {
     int fd;
-    void write_all(const uint8_t* p, size_t n) {
+    bool regular = false;   // a regular file: large writes split over threads with pwrite
+    off_t pos = 0;
+    static void put(int fd, const uint8_t* p, size_t n, off_t at, bool positioned) {
         while (n) {
-            const ssize_t w = ::write(fd, p, n);
+            const ssize_t w = positioned ? ::pwrite(fd, p, n, at) : ::write(fd, p, n);
             if (w < 0) {
                 if (errno == EINTR) continue;
                 run_error(std::string("write failed: ") + strerror(errno));
             }
             p += w;
             n -= (size_t)w;
+            at += w;
         }
+    }
+    void write_all(const uint8_t* p, size_t n) {
+        constexpr size_t kPart = size_t(32) << 20;
+        if (!regular || n < 2 * kPart) {
+            put(fd, p, n, pos, regular);
+            pos += (off_t)n;
+            return;
+        }
+        // page-cache copies of one big write scale with threads (the write order on disk is the
+        // page cache's business; the file's bytes are the same)
+        const size_t parts = std::min<size_t>(8, n / kPart);
+        const size_t each = (n / parts + 4095) & ~size_t(4095);
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < parts; ++i) {
+            const size_t b = i * each;
+            if (b >= n) break;
+            th.emplace_back([=] { put(fd, p + b, std::min(each, n - b), pos + (off_t)b, true); });
+        }
+        put(fd, p, std::min(each, n), pos, true);
+        for (auto& t : th) t.join();
+        pos += (off_t)n;
+    }
+};
+
+// An output buffer that is never zero-filled (a std::vector resize would clear a window's worth
+// of bytes the GPU then overwrites) and keeps its pages between windows.
+struct Buf {
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0, len = 0;
+    void reserve(size_t n) {
+        if (cap >= n) return;
+        p.reset(new uint8_t[n]);
+        cap = n;
     }
 };
 
@@ -213,20 +251,23 @@ struct Strategy {
     }
 
     // A window of whole chunks (the last may be short): outputs concatenated in chunk order.
-    void window(const uint8_t* in, size_t n, size_t cs, std::vector<uint8_t>& out) const {
-        out.clear();
+    // Passthrough and basic are position-wise, so the window's output is the chunk outputs
+    // concatenated (tokenizer.rs:108-124, :129-137).
+    void window(const uint8_t* in, size_t n, size_t cs, Buf& out) const {
+        out.len = 0;
         if (n == 0) return;
-        if (kind == kBpe) {
-            out.resize(2 * n);
-            size_t olen = 0;
-            const int rc = blt_bpe_process_chunks(h, in, n, cs, gpus, out.data(), out.size(), &olen, nullptr);
-            if (rc) run_error(lib_error(rc));
-            out.resize(olen);
+        if (kind == kPassthrough) {
+            out.reserve(n);
+            memcpy(out.p.get(), in, n);
+            out.len = n;
             return;
         }
-        // passthrough and basic are position-wise: the window's output is the chunk outputs
-        // concatenated (tokenizer.rs:108-124, :129-137)
-        chunk(in, n, out);
+        out.reserve(2 * n);
+        size_t olen = 0;
+        const int rc = kind == kBpe ? blt_bpe_process_chunks(h, in, n, cs, gpus, out.p.get(), out.cap, &olen, nullptr)
+                                    : blt_basic_process_chunk(in, n, out.p.get(), out.cap, &olen);
+        if (rc) run_error(lib_error(rc));
+        out.len = olen;
     }
 };
 
@@ -241,25 +282,40 @@ void run_mmap(const Strategy& st, const std::string& path, size_t cs, Sink& sink
         ::close(fd);
         return;
     }
-    void* map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    // MAP_POPULATE maps the whole file up front (fault-around in bulk, no per-page faults while
+    // the GPU copies read it)
+    const bool timing = getenv("BLT_CLI_TIMING") != nullptr;   // phase times on stderr (tools/cli_rate.py)
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_map = now();
+    void* map = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
     if (map == MAP_FAILED) config_error(path + ": mmap failed: " + strerror(errno));
     ::close(fd);
     const uint8_t* in = static_cast<const uint8_t*>(map);
     madvise(map, n, MADV_SEQUENTIAL);
 
-    // windows of whole chunks, about 512 MiB of input each
-    const size_t per = std::max<size_t>(1, (size_t(512) << 20) / cs);
+    // windows of whole chunks, about 256 MiB of input each
+    const size_t per = std::max<size_t>(1, (size_t(256) << 20) / cs);
     const size_t win = per * cs;
-    std::vector<uint8_t> buf[2];
+    Buf buf[2];
     std::thread writer;
+    double t_tok = 0, t_wait = 0, t0 = now();
+    const double t_mapped = t0;
     for (size_t off = 0, k = 0; off < n; off += win, ++k) {
         const size_t len = std::min(win, n - off);
-        std::vector<uint8_t>& out = buf[k & 1];
+        Buf& out = buf[k & 1];
         st.window(in + off, len, cs, out);
+        const double t1 = now();
         if (writer.joinable()) writer.join();   // window k-1 written: its buffer is free
-        writer = std::thread([&sink, &out] { sink.write_all(out.data(), out.size()); });
+        const double t2 = now();
+        t_tok += t1 - t0;
+        t_wait += t2 - t1;
+        t0 = t2;
+        writer = std::thread([&sink, &out] { sink.write_all(out.p.get(), out.len); });
     }
     if (writer.joinable()) writer.join();
+    if (timing)
+        fprintf(stderr, "blt timing: map %.4f s, tokenise %.4f s, writer wait %.4f s, last write %.4f s\n",
+                t_mapped - t_map, t_tok, t_wait, now() - t0);
     munmap(map, n);
 }
 
@@ -340,7 +396,12 @@ void run_stream(const Strategy& st, size_t cs, size_t threads, Sink& sink) {
 
 }  // namespace
 
+static double mono_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int main(int argc, char** argv) {
+    const double t_main = mono_now();
     const Args a = parse_args(argc, argv);
 
     // CoreConfig::new_from_cli (lib.rs:149-174): threads, chunk size string, merges file
@@ -379,15 +440,27 @@ int main(int argc, char** argv) {
     }
     if (a.has_input && ::access(a.input.c_str(), R_OK) != 0) config_error(a.input + ": " + strerror(errno));
     Sink sink{ofd};
+    {
+        struct stat ob;
+        sink.regular = fstat(ofd, &ob) == 0 && S_ISREG(ob.st_mode) && lseek(ofd, 0, SEEK_CUR) == 0;
+    }
     if (a.content_token >= 0) {   // prepend_content_type_token (lib.rs:284-293)
         const uint8_t t[2] = {(uint8_t)(a.content_token >> 8), (uint8_t)a.content_token};
         sink.write_all(t, 2);
     }
+    const double t_run = mono_now();
     if (a.has_input)
         run_mmap(st, a.input, (size_t)cs, sink);
     else
         run_stream(st, (size_t)cs, (size_t)threads, sink);
+    const double t_done = mono_now();
     if (st.h) blt_bpe_destroy(st.h);
+    if (getenv("BLT_CLI_TIMING"))
+        fprintf(stderr, "blt timing: main at %.4f (monotonic), setup %.4f s, run %.4f s, teardown from %.4f\n", t_main,
+                t_run - t_main, t_done - t_run, t_done);
     if (a.has_output && ::close(ofd) != 0) run_error(std::string("close failed: ") + strerror(errno));
-    return 0;
+    // Every byte is written with write()/pwrite() and the output is closed: leave without the
+    // HIP runtime's exit-time teardown of the device contexts and pinned buffers (~0.4 s).
+    fflush(nullptr);
+    _exit(0);
 }
