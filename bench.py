@@ -130,7 +130,15 @@ def main():
     cpu = None
     cpu_opt = None
     exact = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and distributed:
+        # N > 1: the CPU baseline is reported at N = 1 only; rank 0 still checks its shard
+        # bit-exact, with the dense single-pass oracle (outside the timed region)
+        from oracle import oracle as O
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        fast = O.fast_run(merges, host, CHUNK, threads=threads)
+        if fast is not None:
+            exact = bool(np.array_equal(fast, d_out[:2 * tokens].cpu().numpy()))
+    elif rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
         orc = O.COracle(merges)
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))

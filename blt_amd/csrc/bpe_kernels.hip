@@ -1183,6 +1183,11 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 // (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
 constexpr int kRing = 4;
 constexpr uint32_t kWaitLimit = 1u << 22;
+// s_sleep between polls of an LDS flag (units of 64 cycles): every poll is an LDS instruction
+// that competes with the phase-1 table lookups of the waves still in phase 1
+#ifndef BLT_WSLEEP
+#define BLT_WSLEEP 1
+#endif
 // Per-wave phase stamps and look-back timing (tools/tile_timing.py) only in the timing build
 // (-DBLT_TIMING): kept live across the loop they cost scalar registers the kernel has none of.
 #ifdef BLT_TIMING
@@ -1198,6 +1203,15 @@ constexpr int kPrioEmWave = (BLT_PRIO / 100) % 100, kPrioEm = BLT_PRIO % 100;
 #else
 constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
 constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
+#endif
+// Lead wave (experiment): wave kLead runs phase 1 at priority kLeadPrio, so it finishes first
+// and issues the pending tile's look-back sooner; BLT_LEAD = wave * 10 + priority (-1: none).
+#ifndef BLT_LEAD
+#define BLT_LEAD -1
+#endif
+constexpr int kLead = BLT_LEAD < 0 ? -1 : BLT_LEAD / 10, kLeadPrio = BLT_LEAD < 0 ? 0 : BLT_LEAD % 10;
+#ifndef BLT_LBPRIO
+#define BLT_LBPRIO 0
 #endif
 // Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
 // iteration (a whole iteration to land) and claims tickets two tiles ahead (default; BLT_PF=0
@@ -1228,7 +1242,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
             if ((threadIdx.x & 63) == 0) atomicOr(p.ctl + 1, 8u);
             break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(BLT_WSLEEP);
     }
 }
 
@@ -1374,6 +1388,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+            if (kLead >= 0 && wave == (uint32_t)kLead) __builtin_amdgcn_s_setprio(kLeadPrio);
             phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
@@ -1396,6 +1411,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- carry-in and offset of Tp, by the first wave to finish phase 1: its snapshot is
         // the freshest that still lands before the slower waves finish (~0.5 us round trip)
         if (lbw && Tp < ntiles) {
+            if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(BLT_LBPRIO);
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
@@ -1436,6 +1452,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     }
                 }
             }
+            if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(0);
         }
 
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
