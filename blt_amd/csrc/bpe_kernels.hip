@@ -583,6 +583,15 @@ constexpr int kLbWin = 1;                              // look-back windows of 6
 #endif
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
+#ifndef BLT_LBSLEEP
+#define BLT_LBSLEEP 1   // s_sleep before a look-back re-reads a window that was not ready
+#endif
+// Phase 1 skips the lane functions, SGPR carry chain and DPP scan when every lane of the
+// tile's wave range merges all its pairs (a uniform branch; BLT_DP1=0 removes it).
+#ifndef BLT_DP1
+#define BLT_DP1 0
+#endif
+constexpr bool kDenseP1 = BLT_DP1 != 0;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
 static_assert(kGroups <= 64, "one lane per group in the tile resolve");
@@ -772,6 +781,24 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
     // interleave, and lane 63 writes both wave functions after them
     uint64_t wnonid[kS], wcmask[kS];
     uint32_t wincl[kS];
+    uint64_t anynon = 0;
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
+        anynon |= wnonid[j];
+    }
+    if (kDenseP1 && anynon == 0) {
+        // Every lane of every sub-tile merges all 16 pairs (text under a large merge map): each
+        // lane is an identity that lands 8 tokens under either carry-in, so every lane takes the
+        // wave's carry-in and lane l's tokens start at 8 l under both hypotheses.
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+            st.ex[j] = 0x80008u * (uint32_t)lane;
+            st.lw[j] = 2u;
+            wcmask[j] = 0;
+            wincl[j] = 0x80008u * (uint32_t)(lane + 1);
+        }
+    } else {
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t vm = st.mv[j] >> 16;
@@ -787,7 +814,7 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         // carry-out 1) lane's carry runs up through the identity lanes above it and stops at
         // the next non-identity lane, i.e. the carry chain of M + (D << 1); F = lanes at or below
         // the lowest non-identity lane, fed by c.
-        const uint64_t nonid = __ballot(m[j] != 0xFFFFu);
+        const uint64_t nonid = wnonid[j];
         const uint64_t cmask = __ballot(((M >> 31) & 1u) == 0u);   // carry-out 1 (if not identity)
         const uint64_t D = cmask & nonid, Mi = ~nonid, A = D << 1;
         const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
@@ -798,9 +825,9 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         const uint32_t incl = wave_scan(packed);
         st.ex[j] = incl - packed;
         st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
-        wnonid[j] = nonid;
         wcmask[j] = cmask;
         wincl[j] = incl;
+    }
     }
     if (lane == 63) {
 #pragma unroll
@@ -929,7 +956,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 C = 1u; O = 0ull;
                 return;
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (BLT_LBSLEEP) __builtin_amdgcn_s_sleep(BLT_LBSLEEP);
             lb_issue(p, k, lane, s);
             continue;
         }
@@ -1213,6 +1240,13 @@ constexpr int kLead = BLT_LEAD < 0 ? -1 : BLT_LEAD / 10, kLeadPrio = BLT_LEAD < 
 #ifndef BLT_LBPRIO
 #define BLT_LBPRIO 0
 #endif
+// BLT_LEADLB (with BLT_LEAD): the lead wave always takes the look-back and issues its part of the
+// next tile's loads after its status loads (vmcnt is in order: loads issued earlier by the same
+// wave would hold back the status words)
+#ifndef BLT_LEADLB
+#define BLT_LEADLB 0
+#endif
+constexpr bool kLeadLb = BLT_LEADLB != 0 && kLead >= 0;
 // Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
 // iteration (a whole iteration to land) and claims tickets two tiles ahead (default; BLT_PF=0
 // loads each tile after the previous tile's phase 1).
@@ -1366,7 +1400,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-        if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
+        // (kLeadLb: the look-back wave loads its part of Tq after its status loads, so their
+        // in-order vmcnt wait does not cover these)
+        const bool late_q = kLeadLb && wave == (uint32_t)kLead;
+        if (kPf && Tq < ntiles && !late_q) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
@@ -1379,7 +1416,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
-        bool lbw = wave == 0;   // the wave that resolves Tp: the first to finish phase 1
+        bool lbw = kLeadLb ? late_q : wave == 0;   // the wave that resolves Tp: the first to finish phase 1
         if (T < ntiles) {
 #if defined(BLT_EXP) && (BLT_EXP & 16)
             if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
@@ -1395,7 +1432,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
-            lbw = old == (uint32_t)kWaves * (it / kRing);
+            lbw = kLeadLb ? late_q : old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
@@ -1416,6 +1453,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            if (late_q && kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone, it);
@@ -1454,6 +1492,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             }
             if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(0);
         }
+        if (late_q && kPf && Tq < ntiles && Tp >= ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);
 
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
         // T's bytes are consumed: the loads fly during the emission
