@@ -1451,7 +1451,16 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(BLT_LBPRIO);
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
+#if defined(BLT_EXP) && (BLT_EXP & 32768)
+            // timing experiment: no look-back (C, O of a dense text tile; wrong near chunk ends)
+            const bool lb = false;
+            O = (uint64_t)Tp * (kTilePosBytes / 2);
+#else
             const bool lb = Tp > 0;
+#endif
+#if defined(BLT_LBDRAIN)
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // diagnostic: the wave's own loads land first
+#endif
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             if (late_q && kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
