@@ -55,8 +55,24 @@ def build_merges(synth):
     return synth.merges_dict(synth.text_merges_50k(sample, seed=3))
 
 
+def relaunch(n):
+    """`python bench.py --gpus N` outside a launcher: start one process per GPU under
+    torch.distributed.run as a child (nothing here has touched the GPU) and return its exit code."""
+    import subprocess
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args.gpus))
     import torch
     import torch.distributed as dist
 
