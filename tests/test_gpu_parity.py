@@ -182,7 +182,7 @@ def test_multi_gpu_sharding_is_identical():
 
 def test_basic_strategy_sizes():
     rng = np.random.default_rng(1)
-    for n in (1, 15, 16, 17, 4095, 1 << 20, (1 << 20) + 3):
+    for n in (1, 7, 8, 9, 15, 16, 17, 4095, 1 << 20, (1 << 20) + 3, (3 << 20) + 5):
         data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert blt_amd.BasicTokenizationStrategy().process_chunk(data) == O.basic_process_chunk(data)
 
