@@ -83,9 +83,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    torch.cuda.set_device(local)
+    # BLT_BENCH_BACKEND=gloo with BLT_BENCH_DEVICE=0 rehearses the N > 1 path with every rank on one
+    # GPU (RCCL refuses two ranks on one device); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("BLT_BENCH_BACKEND", "nccl")
+    dev = int(os.environ.get("BLT_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     n = args.bytes_per_gpu
     merges = build_merges(synth)
@@ -130,7 +137,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tokens = int(d_off[-1].item())
 
-    elapsed, kern_ms_max = shard.max_over_ranks([elapsed, kern_ms], device="cuda")
+    elapsed, kern_ms_max = shard.max_over_ranks([elapsed, kern_ms], device="cuda" if backend == "nccl" else None)
     ms_per_step = 1000.0 * elapsed / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
 
