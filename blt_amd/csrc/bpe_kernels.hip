@@ -583,15 +583,6 @@ constexpr int kLbWin = 1;                              // look-back windows of 6
 #endif
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
-#ifndef BLT_LBSLEEP
-#define BLT_LBSLEEP 1   // s_sleep before a look-back re-reads a window that was not ready
-#endif
-// Phase 1 skips the lane functions, SGPR carry chain and DPP scan when every lane of the
-// tile's wave range merges all its pairs (a uniform branch; BLT_DP1=0 removes it).
-#ifndef BLT_DP1
-#define BLT_DP1 0
-#endif
-constexpr bool kDenseP1 = BLT_DP1 != 0;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
 static_assert(kGroups <= 64, "one lane per group in the tile resolve");
@@ -781,24 +772,8 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
     // interleave, and lane 63 writes both wave functions after them
     uint64_t wnonid[kS], wcmask[kS];
     uint32_t wincl[kS];
-    uint64_t anynon = 0;
 #pragma unroll
-    for (int j = 0; j < kS; ++j) {
-        wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
-        anynon |= wnonid[j];
-    }
-    if (kDenseP1 && anynon == 0) {
-        // Every lane of every sub-tile merges all 16 pairs (text under a large merge map): each
-        // lane is an identity that lands 8 tokens under either carry-in, so every lane takes the
-        // wave's carry-in and lane l's tokens start at 8 l under both hypotheses.
-#pragma unroll
-        for (int j = 0; j < kS; ++j) {
-            st.ex[j] = 0x80008u * (uint32_t)lane;
-            st.lw[j] = 2u;
-            wcmask[j] = 0;
-            wincl[j] = 0x80008u * (uint32_t)(lane + 1);
-        }
-    } else {
+    for (int j = 0; j < kS; ++j) wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t vm = st.mv[j] >> 16;
@@ -827,7 +802,6 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
         wcmask[j] = cmask;
         wincl[j] = incl;
-    }
     }
     if (lane == 63) {
 #pragma unroll
@@ -956,7 +930,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 C = 1u; O = 0ull;
                 return;
             }
-            if (BLT_LBSLEEP) __builtin_amdgcn_s_sleep(BLT_LBSLEEP);
+            __builtin_amdgcn_s_sleep(1);
             lb_issue(p, k, lane, s);
             continue;
         }
@@ -1210,11 +1184,6 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 // (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
 constexpr int kRing = 4;
 constexpr uint32_t kWaitLimit = 1u << 22;
-// s_sleep between polls of an LDS flag (units of 64 cycles): every poll is an LDS instruction
-// that competes with the phase-1 table lookups of the waves still in phase 1
-#ifndef BLT_WSLEEP
-#define BLT_WSLEEP 1
-#endif
 // Per-wave phase stamps and look-back timing (tools/tile_timing.py) only in the timing build
 // (-DBLT_TIMING): kept live across the loop they cost scalar registers the kernel has none of.
 #ifdef BLT_TIMING
@@ -1231,22 +1200,6 @@ constexpr int kPrioEmWave = (BLT_PRIO / 100) % 100, kPrioEm = BLT_PRIO % 100;
 constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
 constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
 #endif
-// Lead wave (experiment): wave kLead runs phase 1 at priority kLeadPrio, so it finishes first
-// and issues the pending tile's look-back sooner; BLT_LEAD = wave * 10 + priority (-1: none).
-#ifndef BLT_LEAD
-#define BLT_LEAD -1
-#endif
-constexpr int kLead = BLT_LEAD < 0 ? -1 : BLT_LEAD / 10, kLeadPrio = BLT_LEAD < 0 ? 0 : BLT_LEAD % 10;
-#ifndef BLT_LBPRIO
-#define BLT_LBPRIO 0
-#endif
-// BLT_LEADLB (with BLT_LEAD): the lead wave always takes the look-back and issues its part of the
-// next tile's loads after its status loads (vmcnt is in order: loads issued earlier by the same
-// wave would hold back the status words)
-#ifndef BLT_LEADLB
-#define BLT_LEADLB 0
-#endif
-constexpr bool kLeadLb = BLT_LEADLB != 0 && kLead >= 0;
 // Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
 // iteration (a whole iteration to land) and claims tickets two tiles ahead (default; BLT_PF=0
 // loads each tile after the previous tile's phase 1).
@@ -1276,7 +1229,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
             if ((threadIdx.x & 63) == 0) atomicOr(p.ctl + 1, 8u);
             break;
         }
-        __builtin_amdgcn_s_sleep(BLT_WSLEEP);
+        __builtin_amdgcn_s_sleep(1);
     }
 }
 
@@ -1400,10 +1353,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-        // (kLeadLb: the look-back wave loads its part of Tq after its status loads, so their
-        // in-order vmcnt wait does not cover these)
-        const bool late_q = kLeadLb && wave == (uint32_t)kLead;
-        if (kPf && Tq < ntiles && !late_q) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
+        if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
         // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
         // bytes are needed, so claim order stays close to publish order (a tile claimed two
         // iterations ahead lands behind later-claimed ones and stalls their look-backs)
@@ -1416,7 +1366,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
-        bool lbw = kLeadLb ? late_q : wave == 0;   // the wave that resolves Tp: the first to finish phase 1
+        bool lbw = wave == 0;   // the wave that resolves Tp: the first to finish phase 1
         if (T < ntiles) {
 #if defined(BLT_EXP) && (BLT_EXP & 16)
             if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
@@ -1425,14 +1375,13 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            if (kLead >= 0 && wave == (uint32_t)kLead) __builtin_amdgcn_s_setprio(kLeadPrio);
             phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
                 old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = uni(old);
-            lbw = kLeadLb ? late_q : old == (uint32_t)kWaves * (it / kRing);
+            lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                 resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
@@ -1448,7 +1397,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- carry-in and offset of Tp, by the first wave to finish phase 1: its snapshot is
         // the freshest that still lands before the slower waves finish (~0.5 us round trip)
         if (lbw && Tp < ntiles) {
-            if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(BLT_LBPRIO);
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
 #if defined(BLT_EXP) && (BLT_EXP & 32768)
@@ -1458,11 +1406,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 #else
             const bool lb = Tp > 0;
 #endif
-#if defined(BLT_LBDRAIN)
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // diagnostic: the wave's own loads land first
-#endif
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
-            if (late_q && kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone, it);
@@ -1499,9 +1443,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                     }
                 }
             }
-            if (BLT_LBPRIO) __builtin_amdgcn_s_setprio(0);
         }
-        if (late_q && kPf && Tq < ntiles && Tp >= ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);
 
         // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
         // T's bytes are consumed: the loads fly during the emission
