@@ -121,6 +121,30 @@ def test_byte_valued_single_pass(cs):
     assert np.array_equal(lens, elens)
 
 
+@pytest.mark.parametrize("kind", ["random", "text"])
+def test_wrapping_merges_file(tmp_path, kind):
+    """A merges file of 65 537 lines (every byte pair, then one more): the u16 id counter wraps
+    (config_loader.rs:40), so lines 65 280..65 535 map to ids 0..255, which are key components
+    again, and the map needs several passes (tokenizer.rs:63-86) over a 65 536-entry map."""
+    path = str(tmp_path / "wrap.txt")
+    lines = [f"{(i >> 8) & 255} {i & 255}\n" for i in range(65536)] + ["1 2\n"]
+    with open(path, "w") as f:
+        f.write("".join(lines))
+    s = blt_amd.BpeStrategy.from_file(path)
+    m = O.load_bpe_merges_from_path(path)
+    assert s.info()[1] is False
+    rng = np.random.default_rng(65537)
+    if kind == "random":
+        data = rng.integers(0, 256, (1 << 20) + 77, dtype=np.uint8)
+    else:
+        data = synth.text((1 << 20) + 77, seed=4)
+    for cs in (65536, 300001):
+        got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp)
+        assert np.array_equal(lens, elens)
+
+
 def test_chained_map_long():
     m = {(97, 97): 97}  # "aa" -> "a": log2(n) passes
     data = b"a" * 100000 + b"b" + b"a" * 3
