@@ -309,3 +309,47 @@ def test_host_path_pipelined_windows(cs, n):
     exp, elens = O.COracle(m).run(text, cs, threads=8, return_lens=True)
     assert np.array_equal(got, exp)
     assert np.array_equal(lens, elens)
+
+
+def test_concurrent_calls_share_one_handle():
+    """The reference calls one Arc'd strategy from many tokio tasks at once (pipeline.rs:86,
+    :286): 8 host threads call process_chunk / process_chunks on the same handle
+    concurrently (ctypes releases the GIL), each result bit-exact."""
+    import threading
+    text = synth.text(8 << 20, seed=7)
+    m = synth.merges_dict(synth.text_merges_50k(text[: 4 << 20], seed=7))
+    s = blt_amd.BpeStrategy(m)
+    orc = O.COracle(m)
+    rng = np.random.default_rng(8)
+    jobs = []
+    for t in range(8):
+        for k in range(6):
+            n = int(rng.integers(1, 3 << 20))
+            off = int(rng.integers(0, text.size - n))
+            data = text[off:off + n] if (t + k) % 2 else rng.integers(0, 256, n, dtype=np.uint8)
+            jobs.append((t, k, data, int(rng.choice([65536, 262144, 1 << 20]))))
+    errors = []
+
+    def worker(t):
+        try:
+            for (tt, k, data, cs) in jobs:
+                if tt != t:
+                    continue
+                if k % 3 == 2:
+                    got = np.frombuffer(s.process_chunk(data.tobytes()), np.uint8)
+                    exp = np.frombuffer(orc.process_chunk(data.tobytes()), np.uint8)
+                else:
+                    got = s.process_chunks(data, cs)
+                    exp = orc.run(data, cs, threads=2)
+                if not np.array_equal(got, exp):
+                    errors.append((t, k, data.size, cs))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors
