@@ -353,3 +353,16 @@ def test_concurrent_calls_share_one_handle():
         th.join(timeout=100)
     assert not any(th.is_alive() for th in threads)
     assert not errors, errors
+
+
+@pytest.mark.parametrize("cs", [1, 2, 3, 7, 16, 17, 1000, 2047])
+def test_tiny_chunk_sizes(cs):
+    """The library takes any chunk size > 0 (the CLI clamps to >= 256 KiB, chunking.rs:26-62):
+    a chunk end at nearly every position, per-chunk lengths for every chunk."""
+    rng = np.random.default_rng(cs)
+    m = {(a, b): 256 + 26 * (a - 97) + (b - 97) for a in range(97, 123) for b in range(97, 123)}
+    data = rng.integers(97, 123, 50_000 + cs, dtype=np.uint8)
+    got, lens = blt_amd.BpeStrategy(m).process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=4, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
