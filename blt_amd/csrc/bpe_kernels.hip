@@ -562,6 +562,16 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
 #ifndef BLT_WAVES
 #define BLT_WAVES 16
 #endif
+// Cache policy (buffer aux bits) of the input loads and the output stores: nt (2).  Every input
+// byte is read once by one CU and every output byte written once: cfg3 0.604-0.613 -> 0.597-0.599 ms,
+// cfg5 0.815-0.818 -> 0.804 ms (config_rates, same box); cfg2's 100 MiB, replayed back to back,
+// loses its cache residency (0.0937 -> 0.0955 ms).  0 = the default policy.
+#ifndef BLT_LDPOL
+#define BLT_LDPOL 2
+#endif
+#ifndef BLT_STPOL
+#define BLT_STPOL 2
+#endif
 #ifndef BLT_KS
 #define BLT_KS (32 / BLT_WAVES)
 #endif
@@ -1010,7 +1020,7 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
     const uint32_t o = ab + 16u * (uint32_t)lane;
     if (rg == 0) {
-        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, BLT_STPOL);
         return;
     }
     u32x4 Q;   // lane l - 1's tokens
@@ -1018,7 +1028,7 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q)
         Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
     const uint32_t off = 16u - rg;
-    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, 0);
+    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, BLT_STPOL);
     if (lane == 0 || lane == 63) {
         const uint32_t h = 8u - (rg >> 1);   // tokens of this lane in its own block
 #pragma unroll
@@ -1128,7 +1138,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
 #pragma unroll
                 for (int q = 0; q < kCopyBlk; ++q)
                     if ((uint32_t)lane + 64u * q < nfull)
-                        __builtin_amdgcn_raw_buffer_store_b128(vb[q], ro, (int)(abp + hend + 16u * lane + 1024u * q), 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(vb[q], ro, (int)(abp + hend + 16u * lane + 1024u * q), 0, BLT_STPOL);
                 if (bf) __builtin_amdgcn_raw_buffer_store_b16(vf, ro, (int)(abp + of), 0, 0);
             }
         }
@@ -1152,7 +1162,7 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, BLT_LDPOL);
         x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
         // the byte after the range, as its whole (4-aligned) dword: a u8 load would be masked
         // right here, which makes the compiler wait for it.  The range check covers voffset
