@@ -1525,15 +1525,17 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 // Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).  A streaming copy
 // that doubles the bytes: each thread loads one 8-byte input block and writes it as one 16-byte
 // output block, so every store instruction of a wave covers 1 KiB of contiguous output, and the
-// grid has one thread per block (1 GiB: 0.514 ms, 6.26 TB/s algorithmic = 78 % of HBM peak).
+// grid has one thread per block; the stores are non-temporal (1 GiB: 0.493 ms, 6.53 TB/s
+// algorithmic = 82 % of HBM peak).
 // Measured against it: 16-byte loads writing two 16-byte blocks each, 4 in flight per thread
 // over 65,536 workgroups (0.607 ms); 8-byte blocks with 2 or 4 per thread, or fewer workgroups
 // (0.55-0.62 ms).
 #ifndef BLT_BASIC_VEC
 #define BLT_BASIC_VEC 1
 #endif
+// nt stores (2): 0.512-0.514 -> 0.492-0.494 ms per GiB; nt loads (1, 3) less
 #ifndef BLT_BASIC_NT
-#define BLT_BASIC_NT 0
+#define BLT_BASIC_NT 2
 #endif
 #ifndef BLT_BASIC_BLOCKS
 #define BLT_BASIC_BLOCKS (1 << 24)
