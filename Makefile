@@ -1,5 +1,5 @@
 # Builds every native artefact in-tree (they travel to the GPU box with the snapshot).
-#   blt_amd/libblt_bpe.so    product: HIP kernels for gfx950 + C ABI host library
+#   blt_amd/libblt_bpe.so    product: HIP kernels for gfx950 + C ABI host library + pipeline
 #   blt_amd/libblt_synth.so  seeded synthetic workloads (bench / tests)
 #   blt_amd/blt              CLI drop-in for the reference `blt` binary
 #   oracle/liboracle.so      CPU restatement of the reference (test infrastructure only)
@@ -25,7 +25,10 @@ $(OBJDIR)/bpe_kernels.o: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h
 $(OBJDIR)/blt_host.o: blt_amd/csrc/blt_host.cpp blt_amd/csrc/bpe_kernels.h include/blt_bpe.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
-$(LIB): $(OBJDIR)/bpe_kernels.o $(OBJDIR)/blt_host.o
+$(OBJDIR)/blt_pipeline.o: blt_amd/csrc/blt_pipeline.cpp include/blt_bpe.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJDIR)/bpe_kernels.o $(OBJDIR)/blt_host.o $(OBJDIR)/blt_pipeline.o
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -lpthread
 
 # the `blt` command line (src/main.rs drop-in), linked against the library next to it

@@ -13,9 +13,19 @@ path) and `value` is the aggregate input rate: N x 1 GiB / max-over-ranks step t
 Prints ONE JSON line on rank 0.  `roofline` prices the merge-scan kernel alone (HIP events on
 its stream around each launch) against HBM: algorithmic bytes = input bytes + 2 x output
 tokens.  `cpu_baseline` times the C restatement of the reference (hash-map, multi-pass,
-task-per-chunk over all threads) on the same 1 GiB, and its output doubles as the bit-exact
-check of the GPU output; `cpu_baseline_optimized` times a dense-table single-pass CPU version
-beside it.
+task-per-chunk) on the same 1 GiB with one thread per usable host core (num_cpus semantics: the
+cgroup quota, else the affinity mask; both counts are reported), and its output doubles as the
+bit-exact check of the GPU output; `cpu_baseline_optimized` times a dense-table single-pass CPU
+version beside it.
+
+At N = 1 the line also carries (rank 0, outside the timed region of `value`):
+  * `configs`: the other BASELINE workloads on the same kernel, device-resident, kernel-only
+    (median of HIP-event timings), each with its roofline fraction and a bit-exact check:
+    cfg2 (100 MiB text, 256 merges) and cfg5 (1 GiB random bytes, cfg3's 50k merges);
+  * `end_to_end`: cfg3 through blt_bpe_process_chunks from pageable host memory (PCIe-inclusive);
+  * `per_chunk_path`: 16 host threads calling blt_bpe_process_chunk on the 64 16-MiB chunks of
+    cfg3 (the reference's per-chunk strategy calls, pipeline.rs:86, :141-150).
+--workload cfg2|cfg5 makes that workload the timed one (for per-workload rocprofv3 runs).
 """
 import argparse
 import json
@@ -42,10 +52,126 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes-per-gpu", type=int, default=GIB)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("BLT_CPU_THREADS", "16")))
+    ap.add_argument("--no-extra", action="store_true", help="skip configs / end_to_end / per_chunk_path")
+    ap.add_argument("--workload", default="cfg3", choices=["cfg2", "cfg3", "cfg5"])
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("BLT_CPU_THREADS", "0")),
+                    help="0: every usable host core (num_cpus semantics)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
     return ap.parse_args()
+
+
+def usable_cores():
+    """num_cpus::get() as the reference's tokio runtime sizes itself (src/main.rs:81): the cgroup
+    CPU quota if set, else the affinity mask (blt_determine_thread_count(0, 0) computes it the
+    same way); returns (usable, affinity, os.cpu_count())."""
+    from blt_amd import _lib
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return int(_lib.lib().blt_determine_thread_count(0, 0)), aff, os.cpu_count() or 1
+
+
+def kernel_ms(strategy, d_in, n, d_out, reps=20):
+    """Median kernel time (HIP events on the launch stream, workspace reset outside them)."""
+    import torch
+    wsb = strategy.workspace_size(n, CHUNK)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    tok = strategy.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
+    ts = []
+    for _ in range(reps):
+        strategy.workspace_reset(ws.data_ptr(), n, CHUNK, sp)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        strategy.encode_device_prezeroed(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    strategy.check_workspace(ws.data_ptr(), sp)
+    return float(np.median(ts)), tok
+
+
+def workload(synth, name, n):
+    """(host bytes, merges, description) of a BASELINE workload."""
+    if name == "cfg2":
+        host = synth.text(100 << 20, seed=2)
+        return host, synth.merges_dict(synth.top_pair_merges(host, 256)), \
+            "cfg2: 100 MiB synthetic text, 256 merges ranked from it, --chunksize 16MB"
+    merges = build_merges(synth)
+    if name == "cfg5":
+        return synth.random_bytes(n, seed=5), merges, \
+            f"cfg5 (per-GPU share): {n >> 20} MiB random bytes, cfg3's 50000-line merges, --chunksize 16MB"
+    return None, merges, f"cfg3: {n >> 30} GiB synthetic text per GPU, 50000-line merges, --chunksize 16MB"
+
+
+def extra_configs(blt_amd, synth, O, threads):
+    """cfg2 and cfg5 on the same kernel (kernel-only rates, bit-exact against the oracle)."""
+    import torch
+    res = {}
+    for name in ("cfg2", "cfg5"):
+        host, merges, desc = workload(synth, name, GIB)
+        s = blt_amd.BpeStrategy(merges)
+        n = host.size
+        d_in = torch.from_numpy(host).cuda()
+        d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+        ms, tok = kernel_ms(s, d_in, n, d_out)
+        got = d_out[:2 * tok].cpu().numpy()
+        exp = O.COracle(merges).run(host, CHUNK, threads=threads)
+        algo = n + 2 * tok
+        res[name] = {"workload": desc, "bytes": n, "kernel_ms": round(ms, 4),
+                     "input_GBps": round(n / ms / 1e6, 1), "achieved_GBps": round(algo / ms / 1e6, 1),
+                     "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "tokens_per_byte": round(tok / n, 4),
+                     "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
+        del d_in, d_out
+        s.close()
+    return res
+
+
+def host_paths(blt_amd, strategy, host, exp):
+    """PCIe-inclusive rates of the host-buffer entry points on the cfg3 bytes (never `value`)."""
+    import ctypes
+    import threading
+    from blt_amd import _lib
+    L, h, n = _lib.lib(), strategy.handle, host.size
+    out = np.empty(2 * n, np.uint8)
+    olen = ctypes.c_size_t(0)
+    ts = []
+    for _ in range(4):   # the first call pays device allocations and first-touch faults
+        t0 = time.perf_counter()
+        _lib.check(L.blt_bpe_process_chunks(h, host.ctypes.data, n, CHUNK, 1, out.ctypes.data, out.size,
+                                            ctypes.byref(olen), None))
+        ts.append(time.perf_counter() - t0)
+    e2e = {"value": round(n / min(ts[1:]) / 1e9, 3), "unit": "GB/s", "cold_seconds": round(ts[0], 4),
+           "path": "blt_bpe_process_chunks, pageable host in/out, 1 GPU (H2D + kernel + D2H pipelined)",
+           "bit_exact_vs_oracle": bool(np.array_equal(out[:olen.value], exp))}
+    # per-chunk trait path: 16 threads, one process_chunk per 16 MiB chunk
+    nch = n // CHUNK
+    outs = [np.empty(2 * CHUNK, np.uint8) for _ in range(16)]
+    lens = [0] * nch
+    errs = []
+
+    def worker(t):
+        ol = ctypes.c_size_t(0)
+        for k in range(t, nch, 16):
+            rc = L.blt_bpe_process_chunk(h, host.ctypes.data + k * CHUNK, CHUNK, outs[t].ctypes.data, 2 * CHUNK,
+                                         ctypes.byref(ol))
+            if rc:
+                errs.append(rc)
+            lens[k] = ol.value
+    best = None
+    for _ in range(3):
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    per = {"value": round(nch * CHUNK / best / 1e9, 3), "unit": "GB/s", "threads": 16, "chunk_bytes": CHUNK,
+           "chunks": nch, "path": "blt_bpe_process_chunk per 16 MiB chunk from 16 host threads (pageable)",
+           "errors": len(errs), "bytes_match_batched": bool(sum(lens) == olen.value)}
+    return e2e, per
 
 
 def build_merges(synth):
@@ -95,10 +221,14 @@ def main():
             dist.init_process_group(backend)
 
     n = args.bytes_per_gpu
-    merges = build_merges(synth)
+    wl_host, merges, wl_desc = workload(synth, args.workload, n)
     strategy = blt_amd.BpeStrategy(merges)
-    b0, b1 = shard.rank_bytes(world * n, CHUNK, rank, world)   # this rank's chunk range of the stream
-    host = synth.text(b1 - b0, seed=3, offset=b0)
+    if wl_host is None:
+        b0, b1 = shard.rank_bytes(world * n, CHUNK, rank, world)   # this rank's chunk range of the stream
+        host = synth.text(b1 - b0, seed=3, offset=b0)
+    else:
+        host = wl_host
+        n = host.size
     d_in = torch.from_numpy(host).to("cuda")
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     nchunks = (n + CHUNK - 1) // CHUNK
@@ -153,24 +283,27 @@ def main():
     cpu = None
     cpu_opt = None
     exact = None
+    usable, affinity, ncpu = usable_cores()
+    threads = max(1, args.cpu_threads or usable)
+    extras = {}
     if rank == 0 and not args.no_cpu_baseline and distributed:
         # N > 1: the CPU baseline is reported at N = 1 only; rank 0 still checks its shard
         # bit-exact, with the dense single-pass oracle (outside the timed region)
         from oracle import oracle as O
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         fast = O.fast_run(merges, host, CHUNK, threads=threads)
         if fast is not None:
             exact = bool(np.array_equal(fast, d_out[:2 * tokens].cpu().numpy()))
     elif rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
         orc = O.COracle(merges)
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         c0 = time.perf_counter()
         exp = orc.run(host, CHUNK, threads=threads)
         cpu_s = time.perf_counter() - c0
         cpu = {"value": round(n / cpu_s / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-               "sample": f"the same {n >> 20} MiB cfg3 shard, {nchunks} chunks of 16 MiB, C restatement of "
-                         f"tokenizer.rs:56-93 (hash map, multi-pass) on {threads} threads",
+               "usable_cores": usable, "affinity_cpus": affinity, "os_cpu_count": ncpu,
+               "sample": f"the same {n >> 20} MiB {args.workload} shard, {nchunks} chunks of 16 MiB, C restatement "
+                         f"of tokenizer.rs:56-93 (hash map, multi-pass), one task per chunk on {threads} threads "
+                         f"(every usable core: cgroup quota, else affinity mask, as num_cpus)",
                "seconds": round(cpu_s, 3)}
         got = d_out[:2 * tokens].cpu().numpy()
         exact = bool(exp.size == got.size and np.array_equal(exp, got))
@@ -180,17 +313,22 @@ def main():
         fast_s = time.perf_counter() - c0
         if fast is not None:
             cpu_opt = {"value": round(n / fast_s / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port-optimized",
-                       "sample": f"the same {n >> 20} MiB cfg3 shard: dense 64K-entry table, one greedy pass per "
-                                 f"chunk (single-pass map), {threads} threads", "seconds": round(fast_s, 3),
+                       "sample": f"the same {n >> 20} MiB {args.workload} shard: dense 64K-entry table, one greedy "
+                                 f"pass per chunk (single-pass map), {threads} threads", "seconds": round(fast_s, 3),
                        "matches_port": bool(np.array_equal(fast, exp))}
+        if not args.no_extra and args.workload == "cfg3":
+            del d_in, d_out, ws
+            extras["configs"] = extra_configs(blt_amd, synth, O, threads)
+            extras["end_to_end"], extras["per_chunk_path"] = host_paths(blt_amd, strategy, host, exp)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: seeded English-like text (splitmix64, 1 MiB blocks), merges ranked from it",
-            "config": {"workload": "cfg3: 1 GiB synthetic text per GPU, 50000-line merges, --chunksize 16MB",
+            "data": ("synthetic: seeded uniform random bytes (splitmix64), cfg3's merges" if args.workload == "cfg5" else
+                     "synthetic: seeded English-like text (splitmix64, 1 MiB blocks), merges ranked from it"),
+            "config": {"workload": wl_desc,
                        "bytes_per_gpu": n, "chunk_size": CHUNK, "merges": len(merges),
                        "parallelism": f"chunk-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -203,6 +341,7 @@ def main():
             "bit_exact_vs_oracle": exact,
             "output_tokens_per_gpu": tokens,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()

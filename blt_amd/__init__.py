@@ -12,18 +12,25 @@ Python mirror of the reference's strategy surface over the C ABI in include/blt_
   ordered stitch (pipeline.rs:56-192), sharded over GPUs.
 * ``PassthroughStrategy``, ``select_strategy``, ``run_tokenizer`` — strategy choice
   (lib.rs:271-282), content-type token (lib.rs:284-293) and the chunked pipeline over a buffer.
+* ``ByteTokenizer(merges, content_type, threads, chunk_size, memory_cap).tokenize_file(in, out)``,
+  ``load_bpe_merges``, ``version``, ``__version__`` — the reference's Python binding
+  (blt_python/src/lib.rs:27-220, blt_python/python/blt/__init__.py); ``tokenize_file`` runs the
+  file pipeline in the library (``blt_run_tokenizer``, the one the ``blt`` CLI runs).
 
 All tokenising calls run the HIP kernels in libblt_bpe.so; there is no CPU fallback.
 """
 from __future__ import annotations
 
 import ctypes
+import json
+import os
 from typing import Dict, Optional, Tuple
 
 from . import _lib
 from ._lib import BltError
 
 __all__ = [
+    "ByteTokenizer", "__version__", "file_tokenizer",
     "BltError", "TokenizationStrategy", "BpeStrategy", "BasicTokenizationStrategy", "PassthroughStrategy",
     "ContentType", "select_strategy", "run_tokenizer",
     "load_bpe_merges_from_path", "load_bpe_merges", "parse_chunk_size_str", "get_effective_chunk_size",
@@ -32,7 +39,8 @@ __all__ = [
 
 
 def version() -> str:
-    return _lib.lib().blt_version().decode()
+    """version() (blt_python/src/lib.rs:212-215): the library's semantic version."""
+    return _lib.lib().blt_version().decode().split()[-1]
 
 
 class ContentType:
@@ -255,3 +263,110 @@ def run_tokenizer(data, chunk_size: int, strategy: TokenizationStrategy, content
     mv = memoryview(data).cast("B")
     # basic and passthrough are per byte: the chunk split does not change the stream
     return head + strategy.process_chunk(mv) if len(mv) else head
+
+
+def file_tokenizer(input_path: Optional[str], output_path: Optional[str], strategy: Optional[TokenizationStrategy],
+                   content_type: Optional[int], threads: int, chunk_size: int, n_gpus: int = 0) -> None:
+    """run_tokenizer (lib.rs:246-267) over files through the library's pipeline (blt_run_tokenizer):
+    input file (mmap, fixed chunks) or stdin when None, output file (created after the input is
+    opened) or stdout when None, content-type token, chunks in order.  Raises BltError."""
+    cfg = _lib.RunConfig()
+    cfg.input_path = None if input_path is None else os.fsencode(input_path)
+    cfg.output_path = None if output_path is None else os.fsencode(output_path)
+    cfg.passthrough = int(isinstance(strategy, PassthroughStrategy))
+    cfg.bpe = strategy.handle if isinstance(strategy, BpeStrategy) else None
+    cfg.content_token = content_type or 0
+    cfg.threads = max(1, int(threads))
+    cfg.chunk_size = int(chunk_size)
+    cfg.n_gpus = int(n_gpus)
+    _lib.check(_lib.lib().blt_run_tokenizer(ctypes.byref(cfg)))
+
+
+def _u(value, bits: int, name: str) -> int:
+    """PyO3's extraction of a Rust unsigned integer: TypeError for a non-int, OverflowError outside
+    the type's range."""
+    if isinstance(value, bool) or not isinstance(value, int):
+        raise TypeError(f"'{type(value).__name__}' object cannot be interpreted as an integer ({name})")
+    if value < 0 or value >= (1 << bits):
+        raise OverflowError(f"{name} out of range for u{bits}: {value}")
+    return value
+
+
+def _debug_opt(v) -> str:
+    """Rust's {:?} of an Option<String> / Option<int>."""
+    if v is None:
+        return "None"
+    if isinstance(v, str):
+        return "Some(" + json.dumps(v) + ")"
+    return f"Some({v})"
+
+
+class ByteTokenizer:
+    """ByteTokenizer (blt_python/src/lib.rs:27-170) over the MI355X library.
+
+    ``merges``: {(byte1, byte2): token_id}; ``content_type``: "Text" or "Bin" (the reference
+    binding accepts only these two, lib.rs:66-75); ``threads``: chunks in flight; ``chunk_size``:
+    e.g. "16MB" (utils.rs:10-45); ``memory_cap``: percent of RAM for the automatic chunk size
+    (0-100, lib.rs:57-63).
+
+    Documented deviation: the reference writes the dict's KEYS to a temporary merges file in
+    HashMap iteration order (lib.rs:106-113), so its token ids are 256 + that (random) order and the
+    dict's values are ignored; here the ids are the dict's values, deterministically.
+    """
+
+    def __init__(self, merges: Optional[Dict[Tuple[int, int], int]] = None, content_type: Optional[str] = None,
+                 threads: Optional[int] = None, chunk_size: Optional[str] = None, memory_cap: Optional[int] = None):
+        if merges is not None:
+            if not isinstance(merges, dict):
+                raise TypeError("merges must be a dict {(byte1, byte2): token_id}")
+            merges = {(_u(a, 8, "byte1"), _u(b, 8, "byte2")): _u(v, 16, "token_id") for (a, b), v in merges.items()}
+        if threads is not None:
+            threads = _u(threads, 64, "threads")
+        if memory_cap is not None:
+            memory_cap = _u(memory_cap, 8, "memory_cap")
+            if memory_cap > 100:   # lib.rs:57-63
+                raise ValueError("memory_cap must be between 0 and 100")
+        if content_type is not None:
+            if not isinstance(content_type, str):
+                raise TypeError("content_type must be a string")
+            if content_type not in ("Text", "Bin"):   # lib.rs:66-75
+                raise ValueError("content_type must be 'Text' or 'Bin'")
+        if chunk_size is not None and not isinstance(chunk_size, str):
+            raise TypeError("chunk_size must be a string such as '1MB'")
+        self._merges = merges
+        self._content_type = content_type
+        self._threads = threads
+        self._chunk_size = chunk_size
+        self._memory_cap = memory_cap
+
+    def tokenize_file(self, input_path: str, output_path: str) -> None:
+        """lib.rs:90-159: CoreConfig::new_from_cli + run_tokenizer on the two files.  Raises OSError
+        (BltError) on I/O, configuration or GPU failures."""
+        threads = determine_thread_count(self._threads)
+        cli_cs = None
+        if self._chunk_size is not None:
+            out = ctypes.c_uint64(0)
+            L = _lib.lib()
+            rc = L.blt_parse_chunk_size(self._chunk_size.encode(), ctypes.byref(out))
+            if rc:
+                raise BltError(rc, L.blt_last_error().decode())   # io::ErrorKind::InvalidInput
+            cli_cs = out.value
+        mem_cap = 80 if self._memory_cap is None else self._memory_cap   # lib.rs:172
+        cs = get_effective_chunk_size(cli_cs, threads, mem_cap)
+        strategy = BpeStrategy(self._merges) if self._merges is not None else BasicTokenizationStrategy()
+        token = {"Text": ContentType.Text, "Bin": ContentType.Bin}.get(self._content_type)
+        try:
+            file_tokenizer(os.fspath(input_path), os.fspath(output_path), strategy, token, threads, cs)
+        finally:
+            if isinstance(strategy, BpeStrategy):
+                strategy.close()
+
+    def __repr__(self) -> str:   # lib.rs:162-170
+        return (f"ByteTokenizer(merges={len(self._merges) if self._merges is not None else 0}, "
+                f"content_type={_debug_opt(self._content_type)}, threads={_debug_opt(self._threads)}, "
+                f"chunk_size={_debug_opt(self._chunk_size)}, memory_cap={_debug_opt(self._memory_cap)})")
+
+    __str__ = __repr__
+
+
+__version__ = version()

@@ -53,6 +53,13 @@ _u64p = ctypes.POINTER(ctypes.c_uint64)
 _szp = ctypes.POINTER(ctypes.c_size_t)
 _vp = ctypes.c_void_p
 
+class RunConfig(ctypes.Structure):
+    """blt_run_config (include/blt_bpe.h)."""
+    _fields_ = [("input_path", ctypes.c_char_p), ("output_path", ctypes.c_char_p), ("bpe", ctypes.c_void_p),
+                ("passthrough", ctypes.c_int), ("content_token", ctypes.c_uint32), ("threads", ctypes.c_uint64),
+                ("chunk_size", ctypes.c_uint64), ("n_gpus", ctypes.c_int)]
+
+
 _SIGNATURES = {
     "blt_version": (ctypes.c_char_p, []),
     "blt_last_error": (ctypes.c_char_p, []),
@@ -64,6 +71,8 @@ _SIGNATURES = {
     "blt_bpe_create_from_file": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "blt_bpe_destroy": (None, [_vp]),
     "blt_bpe_info": (ctypes.c_int, [_vp, _szp, ctypes.POINTER(ctypes.c_int)]),
+    "blt_bpe_clear_error": (ctypes.c_int, [_vp]),
+    "blt_run_tokenizer": (ctypes.c_int, [ctypes.POINTER(RunConfig)]),
     "blt_bpe_process_chunk": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _szp]),
     "blt_bpe_process_chunks": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _vp,
                                               ctypes.c_size_t, _szp, _vp]),
@@ -76,6 +85,12 @@ _SIGNATURES = {
     "blt_bpe_workspace_reset": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp]),
     "blt_bpe_check_workspace": (ctypes.c_int, [_vp, _vp]),
     "blt_basic_encode_device": (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp]),
+}
+
+# Test hooks exported by the library but not declared in the header.
+_DEBUG_SIGNATURES = {
+    "blt_debug_inject_device_error": (ctypes.c_int, [_vp, _vp, _vp]),
+    "blt_debug_set_tile_record": (None, [_vp]),
 }
 
 
@@ -111,7 +126,7 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is not built: run `make` (or __graft_entry__.build())")
         _share_torch_runtime()
         L = ctypes.CDLL(LIB_PATH)
-        for name, (res, args) in _SIGNATURES.items():
+        for name, (res, args) in list(_SIGNATURES.items()) + list(_DEBUG_SIGNATURES.items()):
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -5,6 +5,8 @@
 // orchestration of the kernels in bpe_kernels.hip, and the multi-GPU chunk sharding that
 // replaces the reference's tokio task-per-chunk pipeline (pipeline.rs:56-192).
 #include <errno.h>
+#include <fcntl.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -15,7 +17,6 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
-#include <fstream>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -40,11 +41,39 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+namespace blt_internal {
+int set_error(int code, const char* fmt, ...) {
+    char buf[2048];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+}  // namespace blt_internal
+
+namespace {
+
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
         hipError_t e_ = (expr);                                                               \
         if (e_ != hipSuccess) return fail(BLT_E_IO, "%s: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
+
+// No C++ exception may cross the C ABI: every int-returning entry point runs its body in GUARDED.
+#define GUARDED(...)                                                                    \
+    try {                                                                               \
+        __VA_ARGS__                                                                     \
+    } catch (const std::bad_alloc&) {                                                   \
+        return fail(BLT_E_NOMEM, "out of host memory");                                 \
+    } catch (const std::exception& e_) {                                                \
+        return fail(BLT_E_IO, "%s", e_.what());                                         \
+    } catch (...) {                                                                     \
+        return fail(BLT_E_IO, "unexpected C++ exception");                              \
+    }
 
 // ---------------------------------------------------------------------------------------
 // Text helpers for the loader: Rust's BufRead::lines() / str::split_whitespace / FromStr.
@@ -125,13 +154,26 @@ const char* parse_unsigned(const std::string& s, uint64_t limit, uint64_t* out) 
 // load_bpe_merges_from_path (config_loader.rs:14-46) into a dense (a, b) -> id table
 // (-1 absent).  Returns 0 or a BLT_E_* code with t_err set to the io::Error text.
 int load_merges_table(const char* path, std::vector<int32_t>& table) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) {
-        const int e = errno ? errno : ENOENT;
+    // File::open + read_line (config_loader.rs:15-21): an OS error is "<strerror> (os error N)"
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) {
+        const int e = errno;
         return fail(e == ENOENT ? BLT_E_NOT_FOUND : BLT_E_IO, "%s (os error %d)", strerror(e), e);
     }
-    std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-    if (f.bad()) return fail(BLT_E_IO, "%s (os error %d)", strerror(EIO), EIO);
+    std::string data;
+    char buf[1 << 16];
+    for (;;) {
+        const ssize_t r = ::read(fd, buf, sizeof buf);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            const int e = errno;   // e.g. EISDIR for a directory
+            ::close(fd);
+            return fail(BLT_E_IO, "%s (os error %d)", strerror(e), e);
+        }
+        if (r == 0) break;
+        data.append(buf, (size_t)r);
+    }
+    ::close(fd);
     table.assign(65536, -1);
     uint16_t vocab = 256;  // :18, wraps like the release build (no overflow-checks)
     size_t pos = 0;
@@ -214,6 +256,12 @@ struct blt_bpe {
     std::vector<uint64_t> hslots;          // general map, empty when single_pass
     uint64_t hmask = 0;
     DevTables dev[kMaxDevices];
+    // Sticky device-error word in pinned, mapped host memory: any kernel of this handle that flags
+    // an error (look-back timeout, output range, prefix invariant) stores 1 here, and every later
+    // call on the handle fails with BLT_E_IO until blt_bpe_clear_error.  An async encode cannot
+    // report its own failure, but the caller's next call does.
+    std::once_flag sticky_once;
+    uint32_t* sticky = nullptr;
 };
 
 namespace {
@@ -324,6 +372,30 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
     return 0;
 }
 
+// The handle's sticky error word (pinned, mapped, portable: one host word every device can
+// store to), allocated on first device use.  nullptr if the allocation failed.
+uint32_t* sticky_word(const blt_bpe* hc) {
+    blt_bpe* h = const_cast<blt_bpe*>(hc);
+    std::call_once(h->sticky_once, [h] {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) == hipSuccess) {
+            memset(p, 0, 64);
+            h->sticky = static_cast<uint32_t*>(p);
+        }
+    });
+    return h->sticky;
+}
+
+// BLT_E_IO if a kernel of this handle flagged a device error since the last blt_bpe_clear_error.
+int sticky_check(const blt_bpe* h) {
+    const uint32_t* w = h->sticky;
+    if (w && __atomic_load_n(w, __ATOMIC_ACQUIRE))
+        return fail(BLT_E_IO,
+                    "a previous merge scan on this handle flagged a device error (look-back timeout, output range "
+                    "or prefix invariant); its output is invalid (blt_bpe_clear_error resets the handle)");
+    return 0;
+}
+
 // Test hook: per-tile look-back records (blt_debug_set_tile_record).
 uint64_t* g_debug_tiles = nullptr;
 
@@ -408,6 +480,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.hmask = h->hmask;
     p.cs_magic = cs ? ~0ull / cs : 0;
     p.debug = g_debug_tiles;
+    p.sticky = h->sticky;
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
@@ -429,6 +502,8 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     if (ws_bytes < L.bytes) return fail(BLT_E_INVALID_INPUT, "workspace too small (%zu < %llu)", ws_bytes, (unsigned long long)L.bytes);
     int dev;
     if (int rc = current_device(&dev)) return rc;
+    if (!sticky_word(h)) return fail(BLT_E_NOMEM, "cannot allocate the pinned error word");
+    if (int rc = sticky_check(h)) return rc;
     DevTables* t;
     if (int rc = device_tables(h, dev, &t)) return rc;
     uint8_t* ws = static_cast<uint8_t*>(d_ws);
@@ -719,13 +794,74 @@ int encode_host_pipelined(const blt_bpe* h, DevCtx* c, const uint8_t* in, uint64
 // ===========================================================================================
 // C ABI
 // ===========================================================================================
+namespace {
+
+// cgroup CPU quota as num_cpus 1.17 reads it (cgroup v2 cpu.max, v1 cfs quota/period): ceil(quota /
+// period), 0 when unlimited or unreadable.
+uint64_t cgroup_cpus() {
+    auto read_two = [](const std::string& path, std::string& a, std::string& b) {
+        FILE* f = fopen(path.c_str(), "r");
+        if (!f) return false;
+        char x[64] = {0}, y[64] = {0};
+        const int k = fscanf(f, "%63s %63s", x, y);
+        fclose(f);
+        if (k < 1) return false;
+        a = x;
+        b = k > 1 ? y : "";
+        return true;
+    };
+    auto ceil_div = [](const std::string& q, const std::string& per) -> uint64_t {
+        char* e1 = nullptr;
+        char* e2 = nullptr;
+        const long long qv = strtoll(q.c_str(), &e1, 10), pv = strtoll(per.c_str(), &e2, 10);
+        if (*e1 || *e2 || qv <= 0 || pv <= 0) return 0;
+        return (uint64_t)((qv + pv - 1) / pv);
+    };
+    // the process's own cgroup (v2: "0::/path")
+    std::string rel;
+    if (FILE* f = fopen("/proc/self/cgroup", "r")) {
+        char line[512];
+        while (fgets(line, sizeof line, f))
+            if (strncmp(line, "0::", 3) == 0) {
+                rel = line + 3;
+                while (!rel.empty() && (rel.back() == '\n' || rel.back() == '\r')) rel.pop_back();
+            }
+        fclose(f);
+    }
+    std::string a, b;
+    for (const std::string& base : {std::string("/sys/fs/cgroup") + (rel == "/" ? "" : rel), std::string("/sys/fs/cgroup")})
+        if (read_two(base + "/cpu.max", a, b)) return a == "max" ? 0 : ceil_div(a, b);
+    std::string q, per, unused;
+    if (read_two("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", q, unused) &&
+        read_two("/sys/fs/cgroup/cpu/cpu.cfs_period_us", per, unused))
+        return ceil_div(q, per);
+    return 0;
+}
+
+// num_cpus::get() (utils.rs:79-97 uses it): the cgroup quota when there is one, otherwise the CPUs
+// this process may run on (sched_getaffinity), otherwise the online CPUs.
+uint64_t available_cpus() {
+    if (const uint64_t q = cgroup_cpus()) return q;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) {
+        const int c = CPU_COUNT(&set);
+        if (c > 0) return (uint64_t)c;
+    }
+    const long c = sysconf(_SC_NPROCESSORS_ONLN);
+    return c > 0 ? (uint64_t)c : 1;
+}
+
+}  // namespace
+
 extern "C" {
 
-const char* blt_version(void) { return "blt-mi355x 0.1.0"; }
+const char* blt_version(void) { return "blt-mi355x 0.2.0"; }
 
 const char* blt_last_error(void) { return t_err.c_str(); }
 
 int blt_load_bpe_merges(const char* path, uint16_t* a, uint16_t* b, uint16_t* v, size_t cap, size_t* n_out) {
+    GUARDED(
     if (!path || !n_out) return fail(BLT_E_INVALID_INPUT, "null argument");
     *n_out = 0;
     std::vector<int32_t> table;
@@ -734,6 +870,7 @@ int blt_load_bpe_merges(const char* path, uint16_t* a, uint16_t* b, uint16_t* v,
     for (int i = 0; i < 65536; ++i) n += table[i] >= 0;
     *n_out = n;
     if (n > cap) return fail(BLT_E_NOSPC, "need room for %zu entries", n);
+    if (n && (!a || !b || !v)) return fail(BLT_E_INVALID_INPUT, "null argument");
     size_t j = 0;
     for (int i = 0; i < 65536; ++i)
         if (table[i] >= 0) {
@@ -743,9 +880,11 @@ int blt_load_bpe_merges(const char* path, uint16_t* a, uint16_t* b, uint16_t* v,
             ++j;
         }
     return 0;
+    )
 }
 
 int blt_parse_chunk_size(const char* str, uint64_t* out) {
+    GUARDED(
     if (!str || !out) return fail(BLT_E_INVALID_INPUT, "null argument");
     // trim (Unicode White_Space, both ends)
     std::string s(str);
@@ -787,6 +926,7 @@ int blt_parse_chunk_size(const char* str, uint64_t* out) {
     if (*parse_unsigned(num, UINT64_MAX, &v)) return fail(BLT_E_INVALID_INPUT, "Invalid number: '%s'", num.c_str());
     *out = v * mult;  // release-build wrapping multiply
     return 0;
+    )
 }
 
 uint64_t blt_effective_chunk_size(int has_cli, uint64_t cli, uint64_t threads, uint32_t memcap) {
@@ -801,21 +941,23 @@ uint64_t blt_effective_chunk_size(int has_cli, uint64_t cli, uint64_t threads, u
 
 uint64_t blt_determine_thread_count(int has_cli, uint64_t threads) {
     if (has_cli) return threads == 0 ? 1 : threads;
-    const long c = sysconf(_SC_NPROCESSORS_ONLN);
-    return c > 0 ? (uint64_t)c : 1;
+    return available_cpus();
 }
 
 int blt_bpe_create(const uint16_t* a, const uint16_t* b, const uint16_t* v, size_t n, uint32_t flags,
                    blt_bpe** out) {
+    GUARDED(
     if (!out || (n && (!a || !b || !v))) return fail(BLT_E_INVALID_INPUT, "null argument");
     if (flags) return fail(BLT_E_INVALID_INPUT, "unknown flags 0x%x", flags);
     std::vector<uint32_t> keys(n);
     std::vector<uint16_t> vals(v, v + n);
     for (size_t i = 0; i < n; ++i) keys[i] = ((uint32_t)a[i] << 16) | b[i];
     return build_handle(keys, vals, out);
+    )
 }
 
 int blt_bpe_create_from_file(const char* path, blt_bpe** out) {
+    GUARDED(
     if (!path || !out) return fail(BLT_E_INVALID_INPUT, "null argument");
     std::vector<int32_t> table;
     if (int rc = load_merges_table(path, table)) {
@@ -828,6 +970,7 @@ int blt_bpe_create_from_file(const char* path, blt_bpe** out) {
     for (uint32_t i = 0; i < 65536; ++i)
         if (table[i] >= 0) { keys.push_back(((i >> 8) << 16) | (i & 255)); vals.push_back((uint16_t)table[i]); }
     return build_handle(keys, vals, out);
+    )
 }
 
 void blt_bpe_destroy(blt_bpe* h) {
@@ -838,6 +981,7 @@ void blt_bpe_destroy(blt_bpe* h) {
         if (h->dev[d].self_be) (void)hipFree(h->dev[d].self_be);
         if (h->dev[d].hslots) (void)hipFree(h->dev[d].hslots);
     }
+    if (h->sticky) (void)hipHostFree(h->sticky);
     delete h;
 }
 
@@ -848,6 +992,13 @@ int blt_bpe_info(const blt_bpe* h, size_t* n_entries, int* single_pass) {
     return 0;
 }
 
+int blt_bpe_clear_error(const blt_bpe* h) {
+    if (!h) return fail(BLT_E_INVALID_INPUT, "null handle");
+    uint32_t* w = h->sticky;
+    if (!w || !__atomic_exchange_n(w, 0u, __ATOMIC_ACQ_REL)) return 0;
+    return fail(BLT_E_IO, "a merge scan on this handle had flagged a device error (now cleared)");
+}
+
 size_t blt_bpe_workspace_size(const blt_bpe* h, uint64_t n, uint64_t cs) {
     if (!h || cs == 0) return 0;
     return (size_t)ws_layout(h->single_pass, n, cs).bytes;
@@ -855,14 +1006,16 @@ size_t blt_bpe_workspace_size(const blt_bpe* h, uint64_t n, uint64_t cs) {
 
 int blt_bpe_encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
                           uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, void* stream, uint64_t* out_tokens) {
-    return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens);
+    GUARDED(return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens);)
 }
 
 int blt_bpe_encode_device_ex(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
                              uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, void* stream, uint64_t* out_tokens,
                              uint32_t flags) {
     if (flags & ~BLT_ENCODE_WORKSPACE_ZEROED) return fail(BLT_E_INVALID_INPUT, "unknown flags 0x%x", flags);
+    GUARDED(
     return encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, (hipStream_t)stream, out_tokens, flags);
+    )
 }
 
 int blt_bpe_workspace_reset(const blt_bpe* h, void* d_ws, uint64_t n, uint64_t cs, void* stream) {
@@ -876,10 +1029,11 @@ int blt_bpe_check_workspace(void* d_ws, void* stream) {
     if (!d_ws) return fail(BLT_E_INVALID_INPUT, "null workspace");
     hipStream_t s = (hipStream_t)stream;
     if (int rc = check_ctl(static_cast<uint8_t*>(d_ws), s)) {
+        const std::string msg = t_err;
         uint32_t z[16] = {0};
         (void)hipMemcpyAsync(d_ws, z, sizeof z, hipMemcpyHostToDevice, s);
         (void)hipStreamSynchronize(s);
-        return rc;
+        return fail(rc, "%s", msg.c_str());
     }
     return 0;
 }
@@ -887,6 +1041,20 @@ int blt_bpe_check_workspace(void* d_ws, void* stream) {
 // Not in the public header: a test hook that makes every merge pass record, per tile, its
 // carry-in/offset/look-back lane and both hypothesis counts into a device buffer.
 void blt_debug_set_tile_record(uint64_t* d_buf) { g_debug_tiles = d_buf; }
+
+// Not in the public header: a test hook that runs the kernels' device-error path (the one a
+// look-back timeout takes) for handle h on the current device and stream, setting error bit 1 in
+// d_ws's control block (nullable) and the handle's sticky word.
+int blt_debug_inject_device_error(const blt_bpe* h, void* d_ws, void* stream) {
+    if (!h) return fail(BLT_E_INVALID_INPUT, "null handle");
+    int dev;
+    if (int rc = current_device(&dev)) return rc;
+    uint32_t* w = sticky_word(h);
+    if (!w) return fail(BLT_E_NOMEM, "cannot allocate the pinned error word");
+    HIP_TRY(blt::launch_inject_error(static_cast<uint32_t*>(d_ws), w, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
 
 int blt_basic_encode_device(const uint8_t* d_in, uint64_t n, uint8_t* d_out, void* stream) {
     if ((!d_in || !d_out) && n) return fail(BLT_E_INVALID_INPUT, "null argument");
@@ -899,8 +1067,10 @@ int blt_basic_encode_device(const uint8_t* d_in, uint64_t n, uint8_t* d_out, voi
 
 int blt_bpe_process_chunk(const blt_bpe* h, const uint8_t* in, size_t n, uint8_t* out, size_t out_cap,
                           size_t* out_len) {
+    GUARDED(
     if (!h || !out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
     *out_len = 0;
+    if (int rc = sticky_check(h)) return rc;
     if (n == 0) return 0;  // tokenizer.rs:57-59
     if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
     int dev;
@@ -909,9 +1079,11 @@ int blt_bpe_process_chunk(const blt_bpe* h, const uint8_t* in, size_t n, uint8_t
     if (int rc = encode_host_on(h, dev, in, n, n, out, &ntok, nullptr)) return rc;
     *out_len = 2 * ntok;
     return 0;
+    )
 }
 
 int blt_basic_process_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, size_t* out_len) {
+    GUARDED(
     if (!out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
     *out_len = 0;
     if (n == 0) return 0;  // tokenizer.rs:109-111
@@ -929,31 +1101,41 @@ int blt_basic_process_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t ou
     HIP_TRY(hipStreamSynchronize(c->stream));
     *out_len = 2 * n;
     return 0;
+    )
 }
 
 int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t cs, int n_gpus, uint8_t* out,
                            size_t out_cap, size_t* out_len, uint64_t* chunk_out_len) {
+    GUARDED(
     if (!h || !out_len || (n && (!in || !out))) return fail(BLT_E_INVALID_INPUT, "null argument");
     if (cs == 0) return fail(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
     *out_len = 0;
+    if (int rc = sticky_check(h)) return rc;
     if (n == 0) return 0;
     if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return fail(BLT_E_NODEV, "no HIP device available");
     const uint64_t nchunks = (n + cs - 1) / cs;
-    uint64_t g = (uint64_t)std::max(1, std::min(n_gpus < 1 ? 1 : n_gpus, std::min(count, kMaxDevices)));
+    // n_gpus shards: contiguous chunk ranges, balanced by chunk count (all chunks but the last are
+    // full); shard r runs on device r % count, so more shards than devices share devices (each
+    // shard its own thread, context and streams)
+    uint64_t g = (uint64_t)std::max(1, std::min(n_gpus < 1 ? 1 : n_gpus, kMaxDevices));
     g = std::min<uint64_t>(g, nchunks);
-    // contiguous chunk ranges, balanced by chunk count (all chunks but the last are full)
     std::vector<uint64_t> c_lo(g + 1);
     for (uint64_t r = 0; r <= g; ++r) c_lo[r] = nchunks * r / g;
     std::vector<uint64_t> tokens(g, 0);
     std::vector<std::vector<uint64_t>> offs(g);
     std::vector<int> rcs(g, 0);
     std::vector<std::string> errs(g);
-    // Each shard is written to its worst-case slot 2 * (first byte) of out, then packed.
+    // each shard writes its worst-case slot 2 * (first byte) of out, then the slots are packed
     auto work = [&](uint64_t r) {
-        const uint64_t b0 = c_lo[r] * cs, b1 = std::min<uint64_t>(c_lo[r + 1] * cs, n);
-        rcs[r] = encode_host_on(h, (int)r, in + b0, b1 - b0, cs, out + 2 * b0, &tokens[r], &offs[r]);
+        try {
+            const uint64_t b0 = c_lo[r] * cs, b1 = std::min<uint64_t>(c_lo[r + 1] * cs, n);
+            rcs[r] = encode_host_on(h, (int)(r % (uint64_t)count), in + b0, b1 - b0, cs, out + 2 * b0, &tokens[r],
+                                    &offs[r]);
+        } catch (const std::exception& e) {
+            rcs[r] = fail(BLT_E_IO, "%s", e.what());
+        }
         if (rcs[r]) errs[r] = t_err;
     };
     if (g == 1) {
@@ -966,7 +1148,9 @@ int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t
         for (uint64_t r = 0; r < g; ++r) th.emplace_back(work, r);
         for (auto& t : th) t.join();
         for (uint64_t r = 0; r < g; ++r)
-            if (rcs[r]) return fail(rcs[r], "device %llu: %s", (unsigned long long)r, errs[r].c_str());
+            if (rcs[r])
+                return fail(rcs[r], "shard %llu (device %llu): %s", (unsigned long long)r,
+                            (unsigned long long)(r % (uint64_t)count), errs[r].c_str());
         // ordered stitch (pipeline.rs:153-168): shards are in chunk order; close the gaps
         uint64_t o = 2 * tokens[0];
         for (uint64_t r = 1; r < g; ++r) {
@@ -983,6 +1167,7 @@ int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t
     }
     *out_len = 2 * total;
     return 0;
+    )
 }
 
 }  // extern "C"

@@ -1,0 +1,397 @@
+// run_tokenizer (blt_core/src/lib.rs:246-267) and the chunked pipeline it drives
+// (blt_core/src/pipeline.rs:22-433) as one C-ABI entry point, blt_run_tokenizer: the `blt` CLI
+// (blt_cli.cpp) and the Python ByteTokenizer.tokenize_file (blt_amd/__init__.py) both call it.
+//
+// Order of effects as in the reference: the input is opened first (io_handler.rs:55-62: File::open
+// + mmap, or stdin), then the output file is created (io_handler.rs:70-78), then the content-type
+// token is written (lib.rs:284-293), then the chunks.  Two input paths (pipeline.rs:22-51):
+//  * a file is mapped and cut into fixed chunk-size chunks (pipeline.rs:73-81); windows of whole
+//    chunks go to blt_bpe_process_chunks / blt_basic_process_chunk (GPU) while the previous window
+//    is written, so the output is the chunk outputs concatenated in chunk order (pipeline.rs:153-192);
+//  * stdin: one read per chunk (pipeline.rs:303-318).  The reference reads through tokio's stdin,
+//    whose blocking adapter (tokio 1.45.1, io/blocking.rs, DEFAULT_MAX_BUF_SIZE) caps one read at
+//    2 MiB, so a chunk is one read(2) of at most min(chunk_size, 2 MiB) bytes; a short read makes a
+//    short chunk.  Up to `threads` chunks are in flight (pipeline.rs:286) and results are written
+//    in chunk order.
+// Every error is returned (first one wins), never exit()ed: 0 or a BLT_E_* code with the message in
+// blt_last_error().
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/blt_bpe.h"
+
+namespace blt_internal {
+int set_error(int code, const char* fmt, ...);
+}
+using blt_internal::set_error;
+
+namespace {
+
+constexpr size_t kStdinReadCap = size_t(2) << 20;   // tokio io::blocking DEFAULT_MAX_BUF_SIZE
+
+// First error of a run wins; later ones are dropped.
+struct RunStatus {
+    std::mutex mu;
+    int rc = 0;
+    std::string msg;
+    void set(int code, const std::string& m) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!rc) { rc = code; msg = m; }
+    }
+    bool failed() {
+        std::lock_guard<std::mutex> g(mu);
+        return rc != 0;
+    }
+};
+
+int os_error(int e) {
+    return set_error(e == ENOENT ? BLT_E_NOT_FOUND : BLT_E_IO, "%s (os error %d)", strerror(e), e);
+}
+
+std::string last_error() {
+    const char* m = blt_last_error();
+    return m ? std::string(m) : std::string();
+}
+
+// Ordered sink over a file descriptor.  Positioned parallel writes only into an output file this
+// run created itself (O_TRUNC, offset 0, nobody else writing it); stdout, whatever it is (pipe,
+// terminal, a shared or O_APPEND file), gets plain sequential write()s, so its file offset advances
+// exactly as the reference's tokio::io::stdout() writes advance it.
+struct Sink {
+    int fd = 1;
+    bool positioned = false;
+    off_t pos = 0;
+    static int put(int fd, const uint8_t* p, size_t n, off_t at, bool positioned) {
+        while (n) {
+            const ssize_t w = positioned ? ::pwrite(fd, p, n, at) : ::write(fd, p, n);
+            if (w < 0) {
+                if (errno == EINTR) continue;
+                return os_error(errno);
+            }
+            p += w;
+            n -= (size_t)w;
+            at += w;
+        }
+        return 0;
+    }
+    int write_all(const uint8_t* p, size_t n) {
+        constexpr size_t kPart = size_t(32) << 20;
+        if (!positioned || n < 2 * kPart) {
+            const int rc = put(fd, p, n, pos, positioned);
+            pos += (off_t)n;
+            return rc;
+        }
+        // page-cache copies of one big write scale with threads
+        const size_t parts = std::min<size_t>(8, n / kPart);
+        const size_t each = (n / parts + 4095) & ~size_t(4095);
+        std::vector<std::thread> th;
+        std::vector<int> rcs(parts, 0);
+        std::vector<std::string> msgs(parts);
+        for (size_t i = 1; i < parts; ++i) {
+            const size_t b = i * each;
+            if (b >= n) break;
+            th.emplace_back([&, i, b] {
+                rcs[i] = put(fd, p + b, std::min(each, n - b), pos + (off_t)b, true);
+                if (rcs[i]) msgs[i] = last_error();
+            });
+        }
+        int rc = put(fd, p, std::min(each, n), pos, true);
+        for (auto& t : th) t.join();
+        for (size_t i = 1; i < parts && !rc; ++i)
+            if (rcs[i]) rc = set_error(rcs[i], "%s", msgs[i].c_str());
+        pos += (off_t)n;
+        return rc;
+    }
+};
+
+// An output buffer that is never zero-filled and keeps its pages between windows.
+struct Buf {
+    std::unique_ptr<uint8_t[]> p;
+    size_t cap = 0, len = 0;
+    void reserve(size_t n) {
+        if (cap >= n) return;
+        p.reset(new uint8_t[n]);
+        cap = n;
+    }
+};
+
+// The per-chunk transform of the selected strategy (lib.rs:271-282, tokenizer.rs:21-31).
+struct Strategy {
+    enum Kind { kPassthrough, kBpe, kBasic } kind;
+    const blt_bpe* h = nullptr;
+    int gpus = 1;
+
+    int chunk(const uint8_t* in, size_t n, std::vector<uint8_t>& out) const {
+        out.clear();
+        if (n == 0) return 0;
+        if (kind == kPassthrough) {
+            out.assign(in, in + n);
+            return 0;
+        }
+        out.resize(2 * n);
+        size_t olen = 0;
+        const int rc = kind == kBpe ? blt_bpe_process_chunk(h, in, n, out.data(), out.size(), &olen)
+                                    : blt_basic_process_chunk(in, n, out.data(), out.size(), &olen);
+        out.resize(rc ? 0 : olen);
+        return rc;
+    }
+
+    // A window of whole chunks (the last may be short), outputs concatenated in chunk order.
+    // Passthrough and basic are position-wise (tokenizer.rs:108-124, :129-137).
+    int window(const uint8_t* in, size_t n, size_t cs, Buf& out) const {
+        out.len = 0;
+        if (n == 0) return 0;
+        if (kind == kPassthrough) {
+            out.reserve(n);
+            memcpy(out.p.get(), in, n);
+            out.len = n;
+            return 0;
+        }
+        out.reserve(2 * n);
+        size_t olen = 0;
+        const int rc = kind == kBpe ? blt_bpe_process_chunks(h, in, n, cs, gpus, out.p.get(), out.cap, &olen, nullptr)
+                                    : blt_basic_process_chunk(in, n, out.p.get(), out.cap, &olen);
+        out.len = rc ? 0 : olen;
+        return rc;
+    }
+};
+
+// mmap path (pipeline.rs:56-192): windows of whole chunks, window k+1 tokenised while window k is
+// written.
+int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& sink) {
+    if (n == 0) return 0;
+    const size_t per = std::max<size_t>(1, (size_t(256) << 20) / cs);   // ~256 MiB of input per window
+    const size_t win = per * cs;
+    Buf buf[2];
+    std::thread writer;
+    int wrc = 0;
+    std::string wmsg;
+    int rc = 0;
+    for (size_t off = 0, k = 0; off < n && !rc; off += win, ++k) {
+        const size_t len = std::min(win, n - off);
+        Buf& out = buf[k & 1];
+        rc = st.window(in + off, len, cs, out);
+        if (writer.joinable()) writer.join();   // window k-1 written: its buffer is free
+        if (wrc) break;
+        if (rc) break;
+        writer = std::thread([&sink, &out, &wrc, &wmsg] {
+            wrc = sink.write_all(out.p.get(), out.len);
+            if (wrc) wmsg = last_error();
+        });
+    }
+    if (writer.joinable()) writer.join();
+    if (rc) return rc;
+    if (wrc) return set_error(wrc, "%s", wmsg.c_str());
+    return 0;
+}
+
+// Stream path (pipeline.rs:196-433): one read per chunk, at most `threads` chunks in flight, a
+// worker pool tokenises (each call stages its chunk through the GPU; the handle is reentrant), a
+// writer emits results in chunk order.  Any error stops reading and is returned.
+int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& sink) {
+    threads = std::max<size_t>(1, threads);
+    const size_t nworkers = std::min<size_t>(threads, 16);
+    const size_t rd = std::min(cs, kStdinReadCap);
+    RunStatus status;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<uint64_t, std::vector<uint8_t>>> jobs;
+    std::map<uint64_t, std::vector<uint8_t>> results;
+    size_t in_flight = 0;   // read, not yet written
+    uint64_t n_read = 0, n_written = 0;
+    bool eof = false, stop = false;
+
+    std::vector<std::thread> pool;
+    for (size_t w = 0; w < nworkers; ++w)
+        pool.emplace_back([&] {
+            for (;;) {
+                std::pair<uint64_t, std::vector<uint8_t>> job;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return !jobs.empty() || eof || stop; });
+                    if (jobs.empty() || stop) return;
+                    job = std::move(jobs.front());
+                    jobs.pop_front();
+                }
+                std::vector<uint8_t> out;
+                const int rc = st.chunk(job.second.data(), job.second.size(), out);
+                std::lock_guard<std::mutex> lk(mu);
+                if (rc) {
+                    status.set(rc, last_error());
+                    stop = true;
+                } else {
+                    results.emplace(job.first, std::move(out));
+                }
+                cv.notify_all();
+            }
+        });
+    std::thread writer([&] {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || results.count(n_written) || (eof && n_written == n_read); });
+            if (stop) return;
+            auto it = results.find(n_written);
+            if (it == results.end()) return;   // eof and everything written
+            std::vector<uint8_t> out = std::move(it->second);
+            results.erase(it);
+            lk.unlock();
+            const int rc = sink.write_all(out.data(), out.size());
+            const std::string m = rc ? last_error() : std::string();
+            lk.lock();
+            if (rc) {
+                status.set(rc, m);
+                stop = true;
+                cv.notify_all();
+                return;
+            }
+            ++n_written;
+            --in_flight;
+            cv.notify_all();
+        }
+    });
+
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return in_flight < threads || stop; });
+            if (stop) break;
+        }
+        std::vector<uint8_t> chunk(rd);
+        ssize_t r;
+        do {
+            r = ::read(in_fd, chunk.data(), rd);
+        } while (r < 0 && errno == EINTR);
+        std::lock_guard<std::mutex> lk(mu);
+        if (r < 0) {
+            status.set(os_error(errno), last_error());
+            stop = true;
+            cv.notify_all();
+            break;
+        }
+        if (r == 0) {
+            eof = true;
+            cv.notify_all();
+            break;
+        }
+        chunk.resize((size_t)r);
+        jobs.emplace_back(n_read++, std::move(chunk));
+        ++in_flight;
+        cv.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        eof = true;
+        cv.notify_all();
+    }
+    for (auto& t : pool) t.join();
+    writer.join();
+    if (status.rc) return set_error(status.rc, "%s", status.msg.c_str());
+    return 0;
+}
+
+int run(const blt_run_config* c) {
+    if (!c) return set_error(BLT_E_INVALID_INPUT, "null config");
+    if (c->chunk_size == 0) return set_error(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
+    if (c->content_token > 0xFFFFu) return set_error(BLT_E_INVALID_INPUT, "content token 0x%x is not a u16", c->content_token);
+    Strategy st;
+    if (c->passthrough) st.kind = Strategy::kPassthrough;   // lib.rs:272-274: passthrough wins
+    else if (c->bpe) st.kind = Strategy::kBpe;
+    else st.kind = Strategy::kBasic;
+    st.h = c->bpe;
+    st.gpus = c->n_gpus;
+    if (st.kind == Strategy::kBpe && st.gpus <= 0) {
+        int count = 0;
+        st.gpus = (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? count : 1;
+    }
+    const size_t cs = (size_t)c->chunk_size;
+
+    // setup_io (io_handler.rs:55-62): the input is opened and mapped first
+    const uint8_t* map = nullptr;
+    size_t n = 0;
+    if (c->input_path) {
+        const int fd = ::open(c->input_path, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) return os_error(errno);
+        struct stat sb;
+        if (fstat(fd, &sb) != 0) {
+            const int e = errno;
+            ::close(fd);
+            return os_error(e);
+        }
+        n = (size_t)sb.st_size;
+        if (n) {
+            // MAP_POPULATE: fault the file in bulk up front, not page by page under the GPU copies
+            void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            if (m == MAP_FAILED) {
+                const int e = errno;
+                ::close(fd);
+                return os_error(e);
+            }
+            madvise(m, n, MADV_SEQUENTIAL);
+            map = static_cast<const uint8_t*>(m);
+        }
+        ::close(fd);
+    }
+    struct Unmap {
+        const uint8_t* p;
+        size_t n;
+        ~Unmap() { if (p) munmap(const_cast<uint8_t*>(p), n); }
+    } unmap{map, n};
+
+    // setup_output_writer (io_handler.rs:70-78): File::create truncates; None is stdout
+    Sink sink;
+    int ofd = 1;
+    if (c->output_path) {
+        ofd = ::open(c->output_path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (ofd < 0) return os_error(errno);
+        sink.fd = ofd;
+        sink.positioned = true;
+    }
+    struct Close {
+        int fd;
+        ~Close() { if (fd > 2) ::close(fd); }
+    } closer{c->output_path ? ofd : -1};
+
+    int rc = 0;
+    if (c->content_token) {   // prepend_content_type_token (lib.rs:284-293)
+        const uint8_t t[2] = {(uint8_t)(c->content_token >> 8), (uint8_t)c->content_token};
+        rc = sink.write_all(t, 2);
+    }
+    if (!rc) {
+        if (c->input_path) rc = run_mmap(st, map, n, cs, sink);
+        else rc = run_stream(st, 0, cs, (size_t)c->threads, sink);
+    }
+    if (!rc && c->output_path) {
+        closer.fd = -1;
+        if (::close(ofd) != 0) rc = os_error(errno);
+    }
+    return rc;
+}
+
+}  // namespace
+
+extern "C" int blt_run_tokenizer(const blt_run_config* cfg) {
+    try {
+        return run(cfg);
+    } catch (const std::bad_alloc&) {
+        return set_error(BLT_E_NOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return set_error(BLT_E_IO, "%s", e.what());
+    }
+}

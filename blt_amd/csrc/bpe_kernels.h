@@ -32,6 +32,8 @@ struct PassParams {
     const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
     uint64_t hmask;
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
+    uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
+                               // error bits in ctl[1], so the handle's next call fails
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
@@ -43,6 +45,8 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
 // hi_merge: every byte-pair merge value is >= 256, so an entry's high byte tells a merge.
 hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
+// Test hook: runs the kernels' error path once (ctl nullable, sticky the handle's error word).
+hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s);
 hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Dense-table layout shared with the host: entry for byte pair (a, b).

@@ -117,10 +117,16 @@ __device__ __forceinline__ uint64_t st_read(const uint64_t* p) {
     return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Error bits into ctl[1] and the handle's sticky host word (vector stores only).
+__device__ __forceinline__ void flag_error(uint32_t* ctl, uint32_t* sticky, uint32_t bit) {
+    if (ctl) atomicOr(ctl + 1, bit);
+    if (sticky) __hip_atomic_store(sticky, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // First failure wins: ctl[2] = T + 1, ctl[3] = sub-tile, ctl[4..5] = O, ctl[6..7] = value, ctl[8] = C.
 __device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint32_t j, uint64_t O, uint64_t v,
                              uint32_t C) {
-    atomicOr(p.ctl + 1, bit);
+    flag_error(p.ctl, p.sticky, bit);
     if (atomicCAS(p.ctl + 2, 0u, T + 1u) == 0u) {
         p.ctl[3] = j;
         p.ctl[4] = (uint32_t)O; p.ctl[5] = (uint32_t)(O >> 32);
@@ -158,9 +164,9 @@ __device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t&
         int f = incl ? (int)__ffsll((unsigned long long)incl) - 1 : 64;
         uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
         if ((ready & need) != need) {
-            if (++spins > kSpinLimit) {
-                if (lane == 0) atomicOr(p.ctl + 1, 1u);
-                C = 1u; O = 0ull;
+            if (++spins > kSpinLimit) {   // flagged; the tile writes nothing (C = 2)
+                if (lane == 0) flag_error(p.ctl, p.sticky, 1u);
+                C = 2u; O = 0ull;
                 return;
             }
             __builtin_amdgcn_s_sleep(2);
@@ -395,13 +401,14 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
                 lookback(p, T, C, O, how);
             }
             if (lane == 0) {
-                const uint64_t end = O + (C ? tf.cnt1 : tf.cnt0);
-                // invariant: a position emits at most one token
-                if (O > tile0 || end > p.n) {
-                    record_error(p, 4u, T, 0xFFu, O, end, C);
-                    O = 0; C = 1;
+                uint64_t end = O + (C ? tf.cnt1 : tf.cnt0);
+                // invariant: a position emits at most one token; a failed tile writes nothing
+                // (C = 2) and publishes a prefix only so its successors finish
+                if (C > 1u || O > tile0 || end > p.n) {
+                    if (C <= 1u) record_error(p, 4u, T, 0xFFu, O, end, C);
+                    O = 0; C = 2u; end = 0;
                 }
-                st_publish(p.status + T, st_incl(C ? co1 : co0, end));
+                st_publish(p.status + T, st_incl(C == 1u ? co1 : co0, end));
                 s_C = C; s_O = O;
                 if (p.debug) {
                     uint64_t* d = p.debug + 4ull * T;
@@ -420,6 +427,7 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
         __syncthreads();
 
         // ---- phase 3: compact and store, one sub-tile at a time ---------------------------
+        if (s_C > 1u) continue;   // failed tile (flagged): no output
         const uint32_t C = s_C;
         const uint64_t O = s_O;
         const uint32_t tile_cnt = C ? s_tfn[3] : s_tfn[2];
@@ -534,6 +542,8 @@ __device__ __forceinline__ uint32_t pk_nz(uint32_t v) {
 }
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef uint32_t __attribute__((aligned(2))) u32_a2;   // LDS takes 2-byte aligned u32 stores (gfx950)
+typedef __attribute__((address_space(3))) u32_a2 lds_u32_a2;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // LDS byte address of a __shared__ object.
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -935,9 +945,9 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
             *bad_out = d;
         }
         if (!ready) {
-            if (++spins > kLbSpinLimit) {
-                if (lane == 0) atomicOr(p.ctl + 1, 1u);
-                C = 1u; O = 0ull;
+            if (++spins > kLbSpinLimit) {   // flagged; the tile writes nothing (C = 2)
+                if (lane == 0) flag_error(p.ctl, p.sticky, 1u);
+                C = 2u; O = 0ull;
                 return;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -1042,6 +1052,105 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
 }
 
 // ---- emission of the pending tile --------------------------------------------------------
+#ifndef BLT_EMIT_IL
+#define BLT_EMIT_IL 0
+#endif
+#ifndef BLT_PAIRW
+#define BLT_PAIRW 0
+#endif
+// Stage layout per wave: kStagePad bytes of slack before the first token (pair writes may store
+// one slot early) and after the last (one slot late); the token at global byte X of a part that
+// starts at the 16-byte boundary abp sits at stage byte kStagePad + X - abp.
+constexpr uint32_t kStagePad = BLT_PAIRW ? 16u : 0u;
+constexpr uint32_t kStageCap = (uint32_t)kStageWave - kStagePad - (BLT_PAIRW ? 16u : 0u);
+
+// A lane's landed tokens into the stage at LDS byte address a, one u16 per position: a consumed
+// position writes the slot the next landing token overwrites.
+__device__ __forceinline__ void stage_b16(const uint32_t (&v)[8], uint32_t L, uint32_t a) {
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const uint32_t tok = v[h];
+        *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
+        add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
+        if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
+        if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
+    }
+}
+
+// The same with one u32 store per position pair (every position of the lane valid).  A pair emits
+// [e(2h), e(2h+1)] (both land), [e(2h)] (2h merges) or [e(2h+1)] (2h was consumed); holes are
+// isolated, so pair h's first token goes to slot s_h = popc(L below 2h+1) - 1 + L[2h] and the
+// pair stores its u32 at slot popc(L & bits 0..2h) - 1: one slot early when 2h was consumed (the
+// low half then lands on pair h-1's last slot) and, when 2h merges, with a junk high half on pair
+// h+1's first slot.  Pairs store in reverse order, so junk low halves are overwritten by the
+// earlier pair's later store; a junk high half is replaced by e(2h+2) (the next pair's first
+// token: 2h+1 was consumed, so 2h+2 lands), except for h = 7, whose slot the next lane stores
+// later.  Pair 0's junk low half would land on the previous lane's last token (stored earlier):
+// it is replaced by that token, e(15) of lane - 1 (merged, since 0 was consumed).
+__device__ __forceinline__ void stage_pairs(const uint32_t (&v)[8], uint32_t L, uint32_t a_first) {
+    const uint32_t prev_hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[7], 0x138, 0xF, 0xF, false) >> 16;
+    const uint32_t a0 = a_first - 2u;   // slot -1
+#pragma unroll
+    for (int h = 7; h >= 0; --h) {
+        uint32_t val = v[h];
+        if (h < 7) {   // high half: e(2h+1) if it lands, else e(2h+2)
+            const uint32_t sel = ((L >> (2 * h + 1)) & 1u) ? 0x07060504u : 0x01000504u;
+            val = __builtin_amdgcn_perm(val, v[h + 1], sel);
+        }
+        if (h == 0) {  // low half: e(0) if it lands, else the previous lane's e(15)
+            val = (L & 1u) ? val : ((val & 0xFFFF0000u) | prev_hi);
+        }
+        const uint32_t a = a0 + 2u * (uint32_t)__popc(L & ((2u << (2 * h)) - 1u));
+        *(lds_u32_a2*)(uintptr_t)a = val;
+    }
+}
+
+// Copy-out of one stage part: whole 16-byte blocks (at most kCopyBlk per lane) and the head and
+// tail fragments (u16 each, lanes 0..7 and 8..15).
+constexpr int kCopyBlk = (kStageWave + 1023) / 1024;
+struct CopyPart {
+    uint32_t abp;    // 16-byte aligned output byte of the part's first block (from obase)
+    uint32_t rgp;    // the part's first token's byte offset from abp (0..15)
+    uint32_t re;     // end of the part's tokens, from abp
+};
+struct CopyData {
+    u32x4 vb[kCopyBlk];
+    uint16_t vf;
+};
+__device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c, int lane, CopyData& d) {
+    const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
+    const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
+    const uint32_t nfull = (tbeg - hend) >> 4;
+    const uint32_t of = lane < 8 ? c.rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+    const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
+    const uint8_t* sp = stg + kStagePad;
+#pragma unroll
+    for (int q = 0; q < kCopyBlk; ++q) {
+        d.vb[q] = (u32x4){0u, 0u, 0u, 0u};
+        if ((uint32_t)lane + 64u * q < nfull) d.vb[q] = *reinterpret_cast<const u32x4*>(sp + hend + 16u * lane + 1024u * q);
+    }
+    d.vf = bf ? reinterpret_cast<const uint16_t*>(sp)[of >> 1] : (uint16_t)0;
+}
+__device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const CopyPart& c, int lane, const CopyData& d) {
+    const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
+    const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
+    const uint32_t nfull = (tbeg - hend) >> 4;
+    const uint32_t of = lane < 8 ? c.rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
+    const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
+#pragma unroll
+    for (int q = 0; q < kCopyBlk; ++q)
+        if ((uint32_t)lane + 64u * q < nfull)
+            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, BLT_STPOL);
+    if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, 0);
+}
+
+// Sparse wave range: per-lane landing mask and token offset, the range's token count.
+struct SparseRange {
+    uint32_t L, lane_off;   // per lane
+    uint32_t gb, wcnt;      // uniform: output byte of the range (from obase), tokens
+    bool full;              // every position of the range is valid (no buffer end)
+};
+
 // Tile-level: carry-in C, O tokens before the tile; the output resource starts at the 16-byte
 // boundary at or below byte 2 O, so every offset below is 32-bit.
 __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, const TInfo& ti, uint32_t cs32,
@@ -1051,10 +1160,11 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
     const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
-    const uint16_t* st16 = reinterpret_cast<const uint16_t*>(stg);
-    const uint32_t stg_lds = lds_addr(stg);
+    const uint32_t stg_lds = lds_addr(stg) + kStagePad;
     uint32_t cnext = ti.bge;   // first chunk start >= the wave range's first position
     uint64_t kc = ti.k0;       // its chunk index
+    SparseRange sr[kS];
+    bool sparse[kS];
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t g = (uint32_t)j * kWaves + wave;
@@ -1062,15 +1172,15 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t cg = uni(gin[g][C]);
         const uint32_t goff = uni(gin[g][2 + C]);          // tokens before this wave range in the tile
         const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
-        const uint32_t ab = gb & ~15u, rg = gb - ab;
         // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
         while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
         const bool cstart = p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos;
-        if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
+        sparse[j] = __ballot(st.mv[j] != 0xFFFFFFFFu) != 0;
+        if (!sparse[j]) {
             // dense: every pair merges, no buffer end, so no chunk end: a chunk can only start at
             // the range's first position
             if (cstart && lane == 0) p.chunk_off[kc] = O + goff;
-            emit_dense(st.v[j], cg, rg, ro, ab, lane);
+            emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
             continue;
         }
         const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
@@ -1081,66 +1191,57 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
         const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
         const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
-        const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
         if (cstart) {
             const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
             if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
+        sr[j].L = L;
+        sr[j].lane_off = lane_off;
+        sr[j].gb = gb;
+        sr[j].wcnt = uni(lane_u32(lane_off + __popc(L), 63));
+        sr[j].full = ti.rn > wrel && ti.rn - wrel >= kWavePos;
+    }
+    auto fits = [&](int j) { return (sr[j].gb & 15u) + 2u * sr[j].wcnt <= kStageCap; };
+    auto stage = [&](int j, uint32_t base) {   // the range's tokens from token `base` on
+        const uint32_t a = stg_lds + (sr[j].gb & 15u) + 2u * (sr[j].lane_off - base);
+        if (BLT_PAIRW && sr[j].full) stage_pairs(st.v[j], sr[j].L, a);
+        else stage_b16(st.v[j], sr[j].L, a);
+    };
+    if (BLT_EMIT_IL && kS == 2 && sparse[0] && sparse[1] && fits(0) && fits(1)) {
+        // both ranges through the stage with their copy-outs interleaved: range 1's stores queue
+        // behind range 0's reads (a wave's LDS operations run in order), so range 0's read latency
+        // is covered by range 1's stage stores
+        CopyPart c0 = {sr[0].gb & ~15u, sr[0].gb & 15u, (sr[0].gb & 15u) + 2u * sr[0].wcnt};
+        CopyPart c1 = {sr[1].gb & ~15u, sr[1].gb & 15u, (sr[1].gb & 15u) + 2u * sr[1].wcnt};
+        CopyData d0, d1;
+        stage(0, 0u);
+        copy_read(stg, c0, lane, d0);
+        stage(1, 0u);
+        copy_read(stg, c1, lane, d1);
+        copy_store(ro, c0, lane, d0);
+        copy_store(ro, c1, lane, d1);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        if (!sparse[j]) continue;
         // Stage -> global in one part, or in two (lanes 0..31, then 32..63: at most 512 tokens
         // each) when the range's tokens overflow the stage (few merges, e.g. random bytes).
-        const uint32_t two = rg + 2u * wcnt > (uint32_t)kStageWave ? 1u : 0u;
-        const uint32_t off32 = two ? uni(lane_u32(lane_off, 32)) : 0u;   // tokens before lane 32
+        const uint32_t two = fits(j) ? 0u : 1u;
+        const uint32_t off32 = two ? uni(lane_u32(sr[j].lane_off, 32)) : 0u;   // tokens before lane 32
         for (uint32_t part = 0; part <= two; ++part) {
             const uint32_t base = part ? off32 : 0u;
-            const uint32_t cnt = two ? (part ? wcnt - off32 : off32) : wcnt;
-            const uint32_t gbp = gb + 2u * base, abp = gbp & ~15u, rgp = gbp - abp;
+            const uint32_t cnt = two ? (part ? sr[j].wcnt - off32 : off32) : sr[j].wcnt;
+            const uint32_t gbp = sr[j].gb + 2u * base;
             if (!two || ((uint32_t)lane >> 5) == part) {
-                uint32_t a = stg_lds + rgp + 2u * (lane_off - base);   // LDS byte address of the next token
-#pragma unroll
-                for (int h = 0; h < 8; ++h) {
-                    const uint32_t tok = st.v[j][h];
-#if defined(BLT_EXP) && (BLT_EXP & 2)
-                    asm volatile("" :: "v"(tok), "v"(a));   // timing experiment: no stage stores
-                    add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
-                    if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
-#else
-                    // a consumed position writes the slot the next landing token overwrites
-                    *(lds_u16*)(uintptr_t)a = (uint16_t)tok;
-                    add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
-                    if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
-                    if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
-#endif
-                }
+                const uint32_t a = stg_lds + (gbp & 15u) + 2u * (sr[j].lane_off - base);
+                if (BLT_PAIRW && sr[j].full && !two) stage_pairs(st.v[j], sr[j].L, a);
+                else stage_b16(st.v[j], sr[j].L, a);
             }
-            // stage -> global: whole 16-byte blocks, then the head and tail fragments (u16 each,
-            // lanes 0..7 and 8..15).  The wave's own LDS writes precede its reads (in-order queue).
-            const uint32_t re = rgp + 2u * cnt;
-            const uint32_t hend = ((rgp + 15u) & ~15u) < re ? ((rgp + 15u) & ~15u) : re;
-            const uint32_t tbeg = (re & ~15u) > hend ? (re & ~15u) : hend;
-            const uint32_t nfull = (tbeg - hend) >> 4;
-            // whole blocks: at most kCopyBlk per lane; all LDS reads issued before the one wait, so
-            // the stage's read latency is paid once
-            constexpr int kCopyBlk = (kStageWave + 1023) / 1024;
-            u32x4 vb[kCopyBlk];
-            const uint32_t of = lane < 8 ? rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
-            const bool bf = lane < 16 && of < (lane < 8 ? hend : re);
-            uint16_t vf = 0;
-#pragma unroll
-            for (int q = 0; q < kCopyBlk; ++q) {
-                vb[q] = (u32x4){0u, 0u, 0u, 0u};
-                if ((uint32_t)lane + 64u * q < nfull) vb[q] = *reinterpret_cast<const u32x4*>(stg + hend + 16u * lane + 1024u * q);
-            }
-            if (bf) vf = st16[of >> 1];
-#if defined(BLT_EXP) && (BLT_EXP & 4)
-            if (nfull == 12345u)   // timing experiment: no copy-out
-#endif
-            {
-#pragma unroll
-                for (int q = 0; q < kCopyBlk; ++q)
-                    if ((uint32_t)lane + 64u * q < nfull)
-                        __builtin_amdgcn_raw_buffer_store_b128(vb[q], ro, (int)(abp + hend + 16u * lane + 1024u * q), 0, BLT_STPOL);
-                if (bf) __builtin_amdgcn_raw_buffer_store_b16(vf, ro, (int)(abp + of), 0, 0);
-            }
+            const CopyPart cp = {gbp & ~15u, gbp & 15u, (gbp & 15u) + 2u * cnt};
+            CopyData d;
+            copy_read(stg, cp, lane, d);
+            copy_store(ro, cp, lane, d);
         }
     }
 }
@@ -1236,7 +1337,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
     uint32_t spins = 0;
     while (lds_acquire(f) < v) {
         if (++spins > kWaitLimit) {
-            if ((threadIdx.x & 63) == 0) atomicOr(p.ctl + 1, 8u);
+            if ((threadIdx.x & 63) == 0) flag_error(p.ctl, p.sticky, 8u);
             break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1424,17 +1525,19 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, kTiming ? &bad : nullptr);
             if (lane == 0) {
-                const uint64_t end = O + (C ? tf3 : tf2);
-                if (O > (uint64_t)Tp * kTilePosBytes || end > n) {
-                    record_error(p, 4u, Tp, 0xFFu, O, end, C);
-                    O = 0; C = 1;
+                const uint64_t end = O + (C == 1u ? tf3 : tf2);
+                // a failed tile (flagged) writes nothing (C = 2) and publishes a prefix only so its
+                // successors finish
+                if (C > 1u || O > (uint64_t)Tp * kTilePosBytes || end > n) {
+                    if (C <= 1u) record_error(p, 4u, Tp, 0xFFu, O, end, C);
+                    O = 0; C = 2u;
                 }
                 // the other waves need only C and O: release them first, publish after
                 s_C[pslot] = C;
                 s_O[pslot] = O;
                 lds_release(&s_lbdone, it + 1u);
-                const uint64_t fin = O + (C ? tf3 : tf2);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C ? tf1 : tf0, fin));
+                const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
                     *p.total = fin;
@@ -1473,8 +1576,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (Tp == kNone - 1u)   // timing experiment: no emission
 #endif
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
-            emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], uni(s_C[pslot]), uni64(s_O[pslot]),
-                      s_stage[wave]);
+            const uint32_t Cp = uni(s_C[pslot]);
+            if (Cp <= 1u)   // C = 2: a failed tile (flagged), no output
+                emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], Cp, uni64(s_O[pslot]), s_stage[wave]);
             __builtin_amdgcn_s_setprio(0);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
@@ -1599,6 +1703,10 @@ __global__ __launch_bounds__(256) void bswap16_kernel(const uint16_t* __restrict
     }
 }
 
+__global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
+    if (threadIdx.x == 0) flag_error(ctl, sticky, 1u);
+}
+
 // ---- launchers ---------------------------------------------------------------------------
 static int grid_for_tiles(uint32_t ntiles, int device, const void* fn) {
     static int cached_cus[64] = {0};
@@ -1661,6 +1769,11 @@ hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipS
     if (blocks < 1) blocks = 1;
     if (blocks > BLT_BASIC_BLOCKS) blocks = BLT_BASIC_BLOCKS;
     hipLaunchKernelGGL(basic_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s) {
+    hipLaunchKernelGGL(inject_error_kernel, dim3(1), dim3(64), 0, s, ctl, sticky);
     return hipGetLastError();
 }
 

@@ -73,7 +73,9 @@ int blt_parse_chunk_size(const char *s, uint64_t *out);
  * otherwise clamp(RAM * memcap% / threads / 4, 1 MiB, 16 MiB) from /proc/meminfo MemTotal. */
 uint64_t blt_effective_chunk_size(int has_cli, uint64_t cli_chunk_size, uint64_t threads, uint32_t memcap_percent);
 
-/* determine_thread_count (utils.rs:79-97): has_cli -> max(threads, 1); else logical CPUs. */
+/* determine_thread_count (utils.rs:79-97): has_cli -> max(threads, 1); else num_cpus::get()
+ * (num_cpus 1.17): the cgroup CPU quota (ceil(quota / period)) if one is set, otherwise the CPUs
+ * in this process's affinity mask. */
 uint64_t blt_determine_thread_count(int has_cli, uint64_t threads);
 
 /* ---------------------------------------------------------------------------------------
@@ -91,6 +93,13 @@ int blt_bpe_create_from_file(const char *merges_path, blt_bpe **out);
 
 void blt_bpe_destroy(blt_bpe *h);
 
+/* Device errors are sticky per handle: when a kernel of h flags an error (look-back timeout,
+ * output range or prefix invariant; its output is then invalid), every later call taking h fails
+ * with BLT_E_IO until this call, which returns BLT_E_IO once if such an error was recorded (and
+ * clears it), 0 otherwise.  The reference's strategy never fails mid-run; a failed GPU run is
+ * reported as the io::Error of the chunk (pipeline.rs:163, :408-414). */
+int blt_bpe_clear_error(const blt_bpe *h);
+
 /* Number of distinct map entries; *single_pass = 1 when one greedy pass is provably the
  * fixpoint (no map value is a key component: true for every merges file below 65 281 lines). */
 int blt_bpe_info(const blt_bpe *h, size_t *n_entries, int *single_pass);
@@ -106,14 +115,36 @@ int blt_bpe_process_chunk(const blt_bpe *h, const uint8_t *in, size_t n, uint8_t
 
 /* The mmap pipeline for a BPE strategy (pipeline.rs:56-192): split in into chunks of
  * chunk_size bytes (pipeline.rs:73-81), tokenise each chunk independently, concatenate in chunk
- * order.  Chunks shard over n_gpus devices (contiguous chunk ranges, no collective); the output
- * is identical for every n_gpus.  chunk_out_len (nullable) receives each chunk's output bytes.
+ * order.  The chunks form n_gpus shards (contiguous chunk ranges, no collective), one host
+ * thread each; shard r runs on device r % (visible devices), so n_gpus above the device count
+ * shares devices.  The output is identical for every n_gpus.  chunk_out_len (nullable) receives each chunk's output bytes.
  * out_cap >= 2 * n. */
 int blt_bpe_process_chunks(const blt_bpe *h, const uint8_t *in, size_t n, size_t chunk_size, int n_gpus,
                            uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *chunk_out_len);
 
 /* BasicTokenizationStrategy::process_chunk (tokenizer.rs:103-124): byte b -> [0, b]. */
 int blt_basic_process_chunk(const uint8_t *in, size_t n, uint8_t *out, size_t out_cap, size_t *out_len);
+
+/* run_tokenizer (lib.rs:246-267) with its pipeline (pipeline.rs:22-433): input file (mmap, fixed
+ * chunks, pipeline.rs:73-81) or stdin (one read per chunk, at most min(chunk_size, 2 MiB) bytes as
+ * tokio's stdin reads), the content-type token, every chunk through the selected strategy
+ * (lib.rs:271-282: passthrough > bpe > basic) and the outputs in chunk order to the output file
+ * (created and truncated after the input is opened, io_handler.rs:55-78) or stdout.  threads and
+ * chunk_size are CoreConfig's resolved values (blt_determine_thread_count,
+ * blt_effective_chunk_size).  Errors are the reference's io::Error texts ("No such file or
+ * directory (os error 2)", ...) with their BLT_E_* kind; the first error of a run is returned. */
+typedef struct blt_run_config {
+    const char *input_path;   /* NULL: stdin */
+    const char *output_path;  /* NULL: stdout */
+    const blt_bpe *bpe;       /* BPE strategy, or NULL for the basic strategy */
+    int passthrough;          /* nonzero: PassthroughStrategy (wins over bpe) */
+    uint32_t content_token;   /* 0: none, else BLT_CONTENT_* written big-endian first */
+    uint64_t threads;         /* chunks in flight (CoreConfig::num_threads, >= 1) */
+    uint64_t chunk_size;      /* effective chunk size in bytes (> 0) */
+    int n_gpus;               /* devices the file path shards each window over; 0 = all visible */
+} blt_run_config;
+
+int blt_run_tokenizer(const blt_run_config *cfg);
 
 /* ---------------------------------------------------------------------------------------
  * Device-resident entry points (inputs already in HBM on the current HIP device).
@@ -123,7 +154,8 @@ int blt_basic_process_chunk(const uint8_t *in, size_t n, uint8_t *out, size_t ou
 size_t blt_bpe_workspace_size(const blt_bpe *h, uint64_t n, uint64_t chunk_size);
 
 /* Whole-buffer BPE over chunks of chunk_size bytes, on the current device and the given HIP
- * stream (NULL = default stream).  d_in: n bytes, 16-byte aligned.  d_out: 2 * n bytes,
+ * stream (NULL = default stream).  Fails with BLT_E_IO while the handle has a sticky device error
+ * (blt_bpe_clear_error).  d_in: n bytes, 16-byte aligned.  d_out: 2 * n bytes,
  * 16-byte aligned; receives the stitched big-endian token stream.  d_chunk_off (nullable):
  * nchunks + 1 u64, the output token index where each chunk starts, [nchunks] = total tokens.
  * d_workspace: blt_bpe_workspace_size() bytes.  out_tokens (nullable): if given, the call
@@ -147,7 +179,8 @@ int blt_bpe_encode_device_ex(const blt_bpe *h, const uint8_t *d_in, uint64_t n, 
 int blt_bpe_workspace_reset(const blt_bpe *h, void *d_workspace, uint64_t n, uint64_t chunk_size, void *stream);
 
 /* Reads and clears the device error flags a previous async encode left in d_workspace
- * (waits for the stream).  0 if clean, BLT_E_IO if a look-back timed out. */
+ * (waits for the stream).  0 if clean, BLT_E_IO if a look-back timed out or a range or prefix
+ * check failed.  (The handle's sticky error, blt_bpe_clear_error, is separate.) */
 int blt_bpe_check_workspace(void *d_workspace, void *stream);
 
 /* Basic strategy on device: d_out[2i] = 0, d_out[2i + 1] = d_in[i]. */

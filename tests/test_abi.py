@@ -18,7 +18,8 @@ def test_library_exports_every_header_symbol():
     assert len(syms) >= 17
     for s in syms:
         assert hasattr(L, s), s
-    assert blt_amd.version().startswith("blt-mi355x")
+    assert L.blt_version().decode().startswith("blt-mi355x ")
+    assert L.blt_version().decode().split()[-1] == blt_amd.version()
 
 
 def test_loader_kats(kats, tmp_path):

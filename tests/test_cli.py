@@ -100,6 +100,50 @@ def test_missing_input_file_fails(tmp_path):
     assert r.returncode == 1
 
 
+def test_missing_input_file_message(tmp_path):   # File::open in setup_io -> main.rs:99-102
+    r = run(["-i", str(tmp_path / "nope"), "-o", str(tmp_path / "out"), "--passthrough"])
+    assert r.returncode == 1
+    assert b"Error running tokenizer: No such file or directory (os error 2)" in r.stderr
+    assert not (tmp_path / "out").exists()   # the output is created after the input is opened
+
+
+def test_dash_is_a_file_name(tmp_path):
+    """clap passes "-" through as a path and File::open / File::create open files named "-"
+    (io_handler.rs:57, :73); the standard streams are used only when -i / -o are absent."""
+    (tmp_path / "-").write_bytes(b"from a file named dash")
+    r = run(["--passthrough", "-i", "-"], b"from stdin", cwd=str(tmp_path))
+    assert r.returncode == 0 and r.stdout == b"from a file named dash"
+    (tmp_path / "-").unlink()
+    r = run(["--passthrough", "-o", "-"], b"to a file named dash", cwd=str(tmp_path))
+    assert r.returncode == 0 and r.stdout == b""
+    assert (tmp_path / "-").read_bytes() == b"to a file named dash"
+
+
+def test_merges_path_is_a_directory(tmp_path):   # read_line -> EISDIR, no abort
+    r = run(["--merges", str(tmp_path), "--passthrough"], b"ab")
+    assert r.returncode == 1
+    assert b"Failed to load BPE merges: Is a directory (os error 21)" in r.stderr
+
+
+def test_stdout_appended_and_shared(tmp_path):
+    """stdout gets sequential write()s: with '>>' the output lands after what the file held, and a
+    later writer of the same open file continues after blt's bytes (the reference's
+    tokio::io::stdout() advances the shared offset the same way)."""
+    data = np.random.default_rng(9).integers(0, 256, (72 << 20) + 3, dtype=np.uint8).tobytes()
+    src, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    src.write_bytes(data)
+    out.write_bytes(b"HEAD")
+    with open(out, "ab") as f:
+        r = subprocess.run([BLT, "--passthrough", "-i", str(src)], stdout=f, stderr=subprocess.PIPE, timeout=300)
+    assert r.returncode == 0
+    assert out.read_bytes() == b"HEAD" + data
+    shared = tmp_path / "shared.bin"
+    r = subprocess.run(f"{{ '{BLT}' --passthrough -i '{src}'; printf TRAILER; }} > '{shared}'", shell=True,
+                       timeout=300)
+    assert r.returncode == 0
+    assert shared.read_bytes() == data + b"TRAILER"
+
+
 @pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU failure")
 def test_tokenising_without_gpu_fails_loudly():
     r = run([], b"hello")
@@ -196,3 +240,35 @@ def test_cli_basic_file_large(tmp_path):
     src.write_bytes(data)
     assert run(["-i", str(src), "-o", str(dst), "--chunksize", "256KB"]).returncode == 0
     assert dst.read_bytes() == basic(data)
+
+
+@pytest.mark.gpu
+def test_cli_stdin_reads_at_most_2mib(tmp_path):
+    """Stream path: the reference reads stdin through tokio, whose blocking adapter caps one read
+    at 2 MiB (tokio 1.45.1 io/blocking.rs DEFAULT_MAX_BUF_SIZE), so with --chunksize 16MB a
+    redirected 5 MiB file is tokenised as 2 MiB chunks (a merge never crosses 2 MiB).  Parity
+    unpinned by the reference's own tests (third-party read size, restated)."""
+    from blt_amd import synth
+    from oracle import oracle as O
+    text = synth.text(5 * (1 << 20) + 777, seed=13)
+    pairs = synth.top_pair_merges(text, 250)
+    m = _merges_file(tmp_path, pairs)
+    merges = {(a, b): 256 + i for i, (a, b) in enumerate(pairs)}
+    src = tmp_path / "in.txt"
+    src.write_bytes(text.tobytes())
+    with open(src, "rb") as f:
+        r = subprocess.run([BLT, "--merges", str(m), "--chunksize", "16MB"], stdin=f, capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == O.COracle(merges).run(text, 2 << 20, threads=4).tobytes()
+    # a stream where the 2 MiB cut shows: "b" + "aa..." merges (1, 2), (3, 4), ... across every
+    # 2 MiB boundary when read whole, not when read 2 MiB at a time
+    data = b"b" + b"a" * (5 << 20)
+    m2 = tmp_path / "aa.txt"
+    m2.write_text("97 97\n")
+    src.write_bytes(data)
+    with open(src, "rb") as f:
+        r = subprocess.run([BLT, "--merges", str(m2), "--chunksize", "16MB"], stdin=f, capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    arr = np.frombuffer(data, np.uint8)
+    assert r.stdout == O.COracle({(97, 97): 256}).run(arr, 2 << 20, threads=4).tobytes()
+    assert r.stdout != O.COracle({(97, 97): 256}).run(arr, 16 << 20, threads=4).tobytes()

@@ -194,14 +194,61 @@ def test_random_bytes_50k_merges():
     assert np.array_equal(got, exp)
 
 
-def test_multi_gpu_sharding_is_identical():
-    """Output is independent of the GPU count (chunks are independent, §8e)."""
-    data = synth.text(5 << 20, seed=4)
+@pytest.mark.parametrize("n_gpus", [2, 3, 8])
+@pytest.mark.parametrize("kind", ["text", "random"])
+def test_multi_gpu_shards_bit_exact(n_gpus, kind):
+    """The multi-device path of blt_bpe_process_chunks (pipeline.rs:141-168's concurrent tasks):
+    n_gpus shards of contiguous chunk ranges, one host thread each, shard r on device r % count
+    (so on a one-GPU box every shard thread really runs, sharing the device), each writing its
+    worst-case output slot, then the memmove stitch in chunk order.  A chunk count that does not
+    divide evenly, an odd chunk size and a short last chunk; output and per-chunk lengths
+    bit-exact against the oracle."""
+    cs = 262147
+    n = 23 * cs + 12345   # 24 chunks: 8 shards of 3, 3 shards of 8, 2 of 12; short last chunk
+    data = synth.text(n, seed=40 + n_gpus) if kind == "text" else synth.random_bytes(n, seed=40 + n_gpus)
+    m = synth.merges_dict(synth.text_merges_50k(synth.text(4 << 20, seed=4), seed=4))
+    s = blt_amd.BpeStrategy(m)
+    got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
+    orc = O.COracle(m)
+    exp = orc.run(data, cs, threads=4)
+    assert np.array_equal(got, exp)
+    elens = np.array([len(orc.process_chunk(data[k * cs:(k + 1) * cs].tobytes())) for k in range(24)])
+    assert np.array_equal(lens, elens)
+    one = s.process_chunks(data, cs, n_gpus=1)
+    assert np.array_equal(one, got)
+
+
+def test_sticky_device_error():
+    """A device error (the path a look-back timeout takes) makes the handle's next call fail with
+    BLT_E_IO, async or not, until blt_bpe_clear_error; the workspace flags are read and cleared by
+    blt_bpe_check_workspace."""
+    import torch
+    from blt_amd import _lib
+    data = synth.text(1 << 20, seed=5)
     m = synth.merges_dict(synth.top_pair_merges(data, 256))
     s = blt_amd.BpeStrategy(m)
-    one = s.process_chunks(data, 262144, n_gpus=1)
-    many = s.process_chunks(data, 262144, n_gpus=8)  # clamps to the devices present
-    assert np.array_equal(one, many)
+    n, cs = data.size, 262144
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    wsb = s.workspace_size(n, cs)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    args = (d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, sp)
+    tok = s.encode_device(*args, sync=True)
+    L = _lib.lib()
+    assert L.blt_debug_inject_device_error(s.handle, ws.data_ptr(), sp) == 0
+    for call in (lambda: s.encode_device(*args, sync=False), lambda: s.encode_device(*args, sync=True),
+                 lambda: s.process_chunk(b"abc"), lambda: s.process_chunks(data, cs)):
+        with pytest.raises(blt_amd.BltError) as e:
+            call()
+        assert e.value.code == _lib.BLT_E_IO and "device error" in str(e.value)
+    with pytest.raises(blt_amd.BltError):
+        s.check_workspace(ws.data_ptr(), sp)   # the workspace's flag (bit 1) ...
+    s.check_workspace(ws.data_ptr(), sp)       # ... read and cleared
+    assert L.blt_bpe_clear_error(s.handle) == _lib.BLT_E_IO   # reports once, clears
+    assert L.blt_bpe_clear_error(s.handle) == 0
+    assert s.encode_device(*args, sync=True) == tok
+    assert np.array_equal(d_out[:2 * tok].cpu().numpy(), O.COracle(m).run(data, cs, threads=4))
 
 
 def test_basic_strategy_sizes():
@@ -366,3 +413,36 @@ def test_tiny_chunk_sizes(cs):
     exp, elens = O.COracle(m).run(data, cs, threads=4, return_lens=True)
     assert np.array_equal(got, exp)
     assert np.array_equal(lens, elens)
+
+
+def test_concurrent_full_size_chunks():
+    """The reference's per-chunk trait path at its real chunk size: 16 host threads each call
+    process_chunk on 16 MiB chunks of one handle at once (pipeline.rs:86, :141-150: up to
+    `threads` tokio tasks, each process_chunk on one mmap chunk), every result bit-exact."""
+    import threading
+    cs = 16 << 20
+    text = synth.text(4 * cs, seed=17)
+    rnd = synth.random_bytes(2 * cs, seed=18)
+    m = synth.merges_dict(synth.text_merges_50k(text[: 8 << 20], seed=17))
+    s = blt_amd.BpeStrategy(m)
+    chunks = [text[k * cs:(k + 1) * cs] for k in range(4)] + [rnd[k * cs:(k + 1) * cs] for k in range(2)]
+    exp = [O.fast_run(m, c, cs, threads=1) for c in chunks]
+    errors = []
+
+    def worker(t):
+        try:
+            for r in range(2):
+                k = (t + r) % len(chunks)
+                got = np.frombuffer(s.process_chunk(chunks[k]), np.uint8)
+                if not np.array_equal(got, exp[k]):
+                    errors.append((t, k))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads)
+    assert not errors, errors
