@@ -46,25 +46,8 @@ clean:
 
 .PHONY: all clean
 
-# Timing experiments (tools/tile_timing.py with BLT_LIB_PATH): kernel variants with parts of
-# the work removed.  Wrong output by construction; never used by the product or the tests.
-EXPS := 1 2 4 256
-exp: $(foreach e,$(EXPS),build/exp/libblt_bpe_exp$(e).so) build/exp/libblt_bpe_timing.so
-# the timing build of the product kernel (tools/tile_timing.py)
-build/exp/libblt_bpe_timing.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
-	mkdir -p build/exp
-	$(HIPCC) $(HIPFLAGS) -DBLT_TIMING -c $< -o build/exp/ktiming.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/exp/ktiming.o $(OBJDIR)/blt_host.o -lpthread
-build/exp/libblt_bpe_exp%.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
-	mkdir -p build/exp
-	$(HIPCC) $(HIPFLAGS) -DBLT_TIMING -DBLT_EXP=$* -c $< -o build/exp/k$*.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/exp/k$*.o $(OBJDIR)/blt_host.o -lpthread
-.PHONY: exp
-# priority sweeps: make prio PRIOS="8010012 ..." (see kPrio* in bpe_kernels.hip)
-PRIOS ?=
-prio: $(foreach e,$(PRIOS),build/exp/libblt_bpe_prio$(e).so)
-build/exp/libblt_bpe_prio%.so: blt_amd/csrc/bpe_kernels.hip blt_amd/csrc/bpe_kernels.h $(OBJDIR)/blt_host.o
-	mkdir -p build/exp
-	$(HIPCC) $(HIPFLAGS) -DBLT_TIMING -DBLT_PRIO=$* -c $< -o build/exp/kp$*.o
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/exp/kp$*.o $(OBJDIR)/blt_host.o -lpthread
-.PHONY: prio
+# The timing build of the product kernel (per-wave phase stamps; tools/tile_timing.py with
+# BLT_LIB_PATH=build/exp/libblt_bpe_timing.so).  Experiment variants: tools/build_variant.sh.
+timing:
+	bash tools/build_variant.sh timing -DBLT_TIMING
+.PHONY: timing

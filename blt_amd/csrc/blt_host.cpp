@@ -479,6 +479,10 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.hslots = t->hslots;
     p.hmask = h->hmask;
     p.cs_magic = cs ? ~0ull / cs : 0;
+    if (cs && cs % blt::kTilePosBytes == 0 && cs / blt::kTilePosBytes < (1ull << 31)) {
+        p.cs_tiles = (uint32_t)(cs / blt::kTilePosBytes);
+        p.cs_tiles_magic = p.cs_tiles > 1 ? (uint32_t)(0xFFFFFFFFull / p.cs_tiles) : 0u;
+    }
     p.debug = g_debug_tiles;
     p.sticky = h->sticky;
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));

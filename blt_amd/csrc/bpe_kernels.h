@@ -32,6 +32,9 @@ struct PassParams {
     const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
     uint64_t hmask;
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
+    uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles
+                               // (below 2^31), else 0
+    uint32_t cs_tiles_magic;   // floor((2^32 - 1) / cs_tiles) (cs_tiles > 1)
     uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
                                // error bits in ctl[1], so the handle's next call fails
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,

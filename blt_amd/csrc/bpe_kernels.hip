@@ -596,11 +596,9 @@ constexpr int kGroups = kS * kWaves;
 // or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
 // in two parts of 32 lanes (at most 512 tokens each).
 constexpr int kStageWave = 1536 * (16 / kWaves);    // the LDS the table leaves, shared by the waves
-#ifdef BLT_LBWIN
-constexpr int kLbWin = BLT_LBWIN;                      // look-back windows of 64 per round trip
-#else
-constexpr int kLbWin = 1;                              // look-back windows of 64 per round trip
-#endif
+// Look-back windows of 64 status words per round trip.  (Measured: 2 or 4 windows cost more
+// through register spills than the extra round trips they save.)
+constexpr int kLbWin = 1;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLbSpinLimit = 1u << 18;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
@@ -625,26 +623,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void* base, uint
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const uint8_t* in, uint64_t base, uint64_t n) {
     return rsrc_at(in + (base < n ? base : 0), base < n ? n - base : 0);
-}
-
-// A lane's 16 bytes at byte `off` of the resource; the byte after the wave's range for lane 63.
-// Full wave ranges take one 16-byte load; the buffer's last wave range takes checked bytes.
-__device__ __forceinline__ void load_sub(__amdgpu_buffer_rsrc_t r, bool full, int lane, uint32_t (&x)[4],
-                                         uint32_t& nxt) {
-    if (full) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, 16 * lane, 0, 0);
-        x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
-    } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            uint32_t d = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                d |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, 16 * lane + 4 * q + b, 0, 0) << (8 * b);
-            x[q] = d;
-        }
-    }
-    nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)kWavePos, 0, 0);
 }
 
 template <int kCtrl, int kRowMask = 0xF>
@@ -686,12 +664,26 @@ struct TInfo {
     uint64_t k0;    // its chunk index
 };
 
-// x / cs by a high multiply with the host's reciprocal (at most two corrections).
+// The chunk geometry of tile T (every wave computes it for its own tiles: SALU work, no LDS).
+// When the chunk size is a whole number of tiles (every chunk size of the configs: 16 MiB = 512
+// tiles), T / (cs / tile) by a 32-bit high multiply with the host's reciprocal and at most two
+// corrections; otherwise tile0 / cs by a 64-bit high multiply.
 __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
     TInfo t;
     const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
     const uint64_t left = p.n > tile0 ? p.n - tile0 : 0;
     t.rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+    if (p.cs_tiles) {
+        const uint32_t d = p.cs_tiles;
+        uint32_t q = d == 1u ? T : __umulhi(T, p.cs_tiles_magic);
+        uint32_t r = T - q * d;
+        if (r >= d) { q += 1u; r -= d; }
+        if (r >= d) { q += 1u; r -= d; }
+        const uint32_t left_tiles = r ? d - r : 0u;   // tiles to the next chunk start
+        t.bge = left_tiles > 2u ? 0x10000u : left_tiles * (uint32_t)kTilePosBytes;
+        t.k0 = (uint64_t)q + (r ? 1u : 0u);
+        return t;
+    }
     uint64_t q = __umul64hi(tile0, p.cs_magic);
     uint64_t r = tile0 - q * p.cs;
     if (r >= p.cs) { q += 1; r -= p.cs; }
@@ -723,19 +715,9 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             const uint32_t lo = x[j][h >> 1], hi = (h >> 1) < 3 ? x[j][(h >> 1) + 1] : nb;
             t0[h] = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
             const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
-#if defined(BLT_EXP) && (BLT_EXP & 1)
-            st.v[j][h] = (t * 0x9E3779B1u) & 0xFF00FF00u;   // timing experiment: no LDS lookups
-#elif defined(BLT_EXP) && (BLT_EXP & 32)
-            // timing experiment: conflict-free lookups (lane l of a 32-lane group reads bank l)
-            const uint32_t cf = tab + 4u * (uint32_t)(lane & 31) + 128u * (uint32_t)h + (t & 0x7000u);
-            const uint32_t va = *(const lds_u16*)(uintptr_t)cf;
-            const uint32_t vb = *(const lds_u16*)(uintptr_t)(cf + 2u);
-            st.v[j][h] = va | (vb << 16);
-#else
             const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
             const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
             st.v[j][h] = __builtin_amdgcn_perm(vb, va, 0x05040100u);   // va | vb << 16, one op
-#endif
         }
         uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
 #pragma unroll
@@ -1052,20 +1034,10 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
 }
 
 // ---- emission of the pending tile --------------------------------------------------------
-#ifndef BLT_EMIT_IL
-#define BLT_EMIT_IL 0
-#endif
-#ifndef BLT_PAIRW
-#define BLT_PAIRW 0
-#endif
-// Stage layout per wave: kStagePad bytes of slack before the first token (pair writes may store
-// one slot early) and after the last (one slot late); the token at global byte X of a part that
-// starts at the 16-byte boundary abp sits at stage byte kStagePad + X - abp.
-constexpr uint32_t kStagePad = BLT_PAIRW ? 16u : 0u;
-constexpr uint32_t kStageCap = (uint32_t)kStageWave - kStagePad - (BLT_PAIRW ? 16u : 0u);
-
 // A lane's landed tokens into the stage at LDS byte address a, one u16 per position: a consumed
-// position writes the slot the next landing token overwrites.
+// position writes the slot the next landing token overwrites.  (Measured and rejected: one
+// 2-byte-aligned u32 store per position pair, junk halves resolved by store order: bit-exact, but
+// unaligned LDS stores run 2x slower on cfg5 and cfg2.)
 __device__ __forceinline__ void stage_b16(const uint32_t (&v)[8], uint32_t L, uint32_t a) {
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
@@ -1074,34 +1046,6 @@ __device__ __forceinline__ void stage_b16(const uint32_t (&v)[8], uint32_t L, ui
         add2(a, __builtin_amdgcn_ubfe(L, 2 * h, 1));
         if (h < 7 || ((L >> 15) & 1u)) *(lds_u16*)(uintptr_t)a = (uint16_t)(tok >> 16);
         if (h < 7) add2(a, __builtin_amdgcn_ubfe(L, 2 * h + 1, 1));
-    }
-}
-
-// The same with one u32 store per position pair (every position of the lane valid).  A pair emits
-// [e(2h), e(2h+1)] (both land), [e(2h)] (2h merges) or [e(2h+1)] (2h was consumed); holes are
-// isolated, so pair h's first token goes to slot s_h = popc(L below 2h+1) - 1 + L[2h] and the
-// pair stores its u32 at slot popc(L & bits 0..2h) - 1: one slot early when 2h was consumed (the
-// low half then lands on pair h-1's last slot) and, when 2h merges, with a junk high half on pair
-// h+1's first slot.  Pairs store in reverse order, so junk low halves are overwritten by the
-// earlier pair's later store; a junk high half is replaced by e(2h+2) (the next pair's first
-// token: 2h+1 was consumed, so 2h+2 lands), except for h = 7, whose slot the next lane stores
-// later.  Pair 0's junk low half would land on the previous lane's last token (stored earlier):
-// it is replaced by that token, e(15) of lane - 1 (merged, since 0 was consumed).
-__device__ __forceinline__ void stage_pairs(const uint32_t (&v)[8], uint32_t L, uint32_t a_first) {
-    const uint32_t prev_hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[7], 0x138, 0xF, 0xF, false) >> 16;
-    const uint32_t a0 = a_first - 2u;   // slot -1
-#pragma unroll
-    for (int h = 7; h >= 0; --h) {
-        uint32_t val = v[h];
-        if (h < 7) {   // high half: e(2h+1) if it lands, else e(2h+2)
-            const uint32_t sel = ((L >> (2 * h + 1)) & 1u) ? 0x07060504u : 0x01000504u;
-            val = __builtin_amdgcn_perm(val, v[h + 1], sel);
-        }
-        if (h == 0) {  // low half: e(0) if it lands, else the previous lane's e(15)
-            val = (L & 1u) ? val : ((val & 0xFFFF0000u) | prev_hi);
-        }
-        const uint32_t a = a0 + 2u * (uint32_t)__popc(L & ((2u << (2 * h)) - 1u));
-        *(lds_u32_a2*)(uintptr_t)a = val;
     }
 }
 
@@ -1123,7 +1067,7 @@ __device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c,
     const uint32_t nfull = (tbeg - hend) >> 4;
     const uint32_t of = lane < 8 ? c.rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
     const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
-    const uint8_t* sp = stg + kStagePad;
+    const uint8_t* sp = stg;
 #pragma unroll
     for (int q = 0; q < kCopyBlk; ++q) {
         d.vb[q] = (u32x4){0u, 0u, 0u, 0u};
@@ -1148,7 +1092,6 @@ __device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const Copy
 struct SparseRange {
     uint32_t L, lane_off;   // per lane
     uint32_t gb, wcnt;      // uniform: output byte of the range (from obase), tokens
-    bool full;              // every position of the range is valid (no buffer end)
 };
 
 // Tile-level: carry-in C, O tokens before the tile; the output resource starts at the 16-byte
@@ -1160,7 +1103,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
     const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
-    const uint32_t stg_lds = lds_addr(stg) + kStagePad;
+    const uint32_t stg_lds = lds_addr(stg);
     uint32_t cnext = ti.bge;   // first chunk start >= the wave range's first position
     uint64_t kc = ti.k0;       // its chunk index
     SparseRange sr[kS];
@@ -1199,29 +1142,8 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         sr[j].lane_off = lane_off;
         sr[j].gb = gb;
         sr[j].wcnt = uni(lane_u32(lane_off + __popc(L), 63));
-        sr[j].full = ti.rn > wrel && ti.rn - wrel >= kWavePos;
     }
-    auto fits = [&](int j) { return (sr[j].gb & 15u) + 2u * sr[j].wcnt <= kStageCap; };
-    auto stage = [&](int j, uint32_t base) {   // the range's tokens from token `base` on
-        const uint32_t a = stg_lds + (sr[j].gb & 15u) + 2u * (sr[j].lane_off - base);
-        if (BLT_PAIRW && sr[j].full) stage_pairs(st.v[j], sr[j].L, a);
-        else stage_b16(st.v[j], sr[j].L, a);
-    };
-    if (BLT_EMIT_IL && kS == 2 && sparse[0] && sparse[1] && fits(0) && fits(1)) {
-        // both ranges through the stage with their copy-outs interleaved: range 1's stores queue
-        // behind range 0's reads (a wave's LDS operations run in order), so range 0's read latency
-        // is covered by range 1's stage stores
-        CopyPart c0 = {sr[0].gb & ~15u, sr[0].gb & 15u, (sr[0].gb & 15u) + 2u * sr[0].wcnt};
-        CopyPart c1 = {sr[1].gb & ~15u, sr[1].gb & 15u, (sr[1].gb & 15u) + 2u * sr[1].wcnt};
-        CopyData d0, d1;
-        stage(0, 0u);
-        copy_read(stg, c0, lane, d0);
-        stage(1, 0u);
-        copy_read(stg, c1, lane, d1);
-        copy_store(ro, c0, lane, d0);
-        copy_store(ro, c1, lane, d1);
-        return;
-    }
+    auto fits = [&](int j) { return (sr[j].gb & 15u) + 2u * sr[j].wcnt <= (uint32_t)kStageWave; };
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         if (!sparse[j]) continue;
@@ -1234,9 +1156,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             const uint32_t cnt = two ? (part ? sr[j].wcnt - off32 : off32) : sr[j].wcnt;
             const uint32_t gbp = sr[j].gb + 2u * base;
             if (!two || ((uint32_t)lane >> 5) == part) {
-                const uint32_t a = stg_lds + (gbp & 15u) + 2u * (sr[j].lane_off - base);
-                if (BLT_PAIRW && sr[j].full && !two) stage_pairs(st.v[j], sr[j].L, a);
-                else stage_b16(st.v[j], sr[j].L, a);
+                stage_b16(st.v[j], sr[j].L, stg_lds + (gbp & 15u) + 2u * (sr[j].lane_off - base));
             }
             const CopyPart cp = {gbp & ~15u, gbp & 15u, (gbp & 15u) + 2u * cnt};
             CopyData d;
@@ -1302,30 +1222,12 @@ constexpr bool kTiming = true;
 #else
 constexpr bool kTiming = false;
 #endif
-// Wave priorities (s_setprio) during phase 1 and emission: waves >= k*Wave get k*.  BLT_PRIO
-// (timing sweeps only) = P1 wave * 1e6 + P1 priority * 1e4 + emission wave * 100 + priority.
-#ifdef BLT_PRIO
-constexpr int kPrioP1Wave = BLT_PRIO / 1000000, kPrioP1 = (BLT_PRIO / 10000) % 100;
-constexpr int kPrioEmWave = (BLT_PRIO / 100) % 100, kPrioEm = BLT_PRIO % 100;
-#else
+// Wave priorities (s_setprio) during phase 1 and emission: waves >= k*Wave get k*.  The SIMD
+// arbiter favours old waves, so without help the youngest waves finish phase 1 last (holding back
+// the tile's resolve and the aggregate that other workgroups' look-backs wait for) and emission
+// last (holding back their next phase 1); no priorities at all cost 20 %.
 constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
 constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
-#endif
-// Input prefetch distance: kPf loads the bytes of the tile after T at the start of T's
-// iteration (a whole iteration to land) and claims tickets two tiles ahead (default; BLT_PF=0
-// loads each tile after the previous tile's phase 1).
-#ifdef BLT_PF
-constexpr bool kPf = BLT_PF != 0;
-#else
-constexpr bool kPf = true;
-#endif
-// Ticket distance: kTk2 claims the tile after next at the start of each iteration (a whole
-// iteration for the device-scope atomic to return); kPf implies it.
-#ifdef BLT_TK2
-constexpr bool kTk2 = kPf || BLT_TK2 != 0;
-#else
-constexpr bool kTk2 = kPf;
-#endif
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
     return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1344,6 +1246,14 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
     }
 }
 
+// The merge scan over a whole buffer (see the block comment of namespace seg).  Per iteration
+// a workgroup holds three tiles: T (phase 1 now; its bytes were loaded during the previous
+// iteration), Tp (pending emission: its carry-in and offset come from the look-back) and Tq (the
+// next T: its bytes are loaded now, a whole iteration ahead).  The ticket after Tq is claimed
+// at the start of the iteration by one lane (tid 64) and handed over at the end of the claiming
+// wave's emission (a whole iteration for the device-scope atomic to return).  (Measured: the
+// claiming lane computing the claimed tile's chunk geometry once for all waves and publishing it
+// with the ticket delays the hand-over, and cfg3 loses 2 %.)
 template <bool kBE, bool kHiM>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
@@ -1352,13 +1262,13 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
     __shared__ uint32_t s_tfn[kRing][4];            // tile co0, co1, tot0, tot1
     __shared__ uint64_t s_O[kRing];                 // tokens before the tile
-    __shared__ uint32_t s_C[kRing];                 // carry into the tile
-    __shared__ uint32_t s_ticket[kRing];
+    __shared__ uint32_t s_C[kRing];                 // carry into the tile (2: failed tile, no output)
+    __shared__ uint32_t s_tk[kRing];        // claimed tickets
     __shared__ uint32_t s_p1cnt[kRing];     // phase-1 arrivals per slot (kWaves per use); waves
-                                                    // drift across iterations, so one counter would mix them
+                                            // drift across iterations, so one counter would mix them
     __shared__ uint32_t s_rdone;            // iterations whose tile is resolved
     __shared__ uint32_t s_lbdone;           // iterations whose pending tile has C, O
-    __shared__ uint32_t s_tkdone;           // iterations whose next ticket is in s_ticket
+    __shared__ uint32_t s_tkdone;           // iterations whose next ticket is in s_tk
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1368,16 +1278,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
     if (tid == 0) {
-#if defined(BLT_EXP) && (BLT_EXP & 256)
-        s_ticket[0] = blockIdx.x;                 // timing experiment: static round-robin tiles
-#else
-        s_ticket[0] = atomicAdd(p.ctl, 1u);
-#endif
-#if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (kTk2) s_ticket[1] = s_ticket[0] + gridDim.x;
-#else
-        if (kTk2) s_ticket[1] = atomicAdd(p.ctl, 1u);   // the tile after it
-#endif
+        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);   // T
+        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);   // Tq, the tile after it
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
@@ -1388,100 +1290,42 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
-#if defined(BLT_EXP) && (BLT_EXP & 16384)
-    {   // timing experiment: the memory traffic alone (read a tile, write 32 KiB), static tiles,
-        // the next tile's bytes prefetched one tile ahead
-        uint32_t xa[kS][4], na[kS];
-        const __amdgpu_buffer_rsrc_t ro = rsrc_at(p.out, p.out_cap);
-        uint32_t Ta = blockIdx.x;
-        if (Ta < ntiles) load_tile(p, Ta, wave, lane, xa, na);
-        for (; Ta < ntiles; Ta += gridDim.x) {
-            uint32_t xb[kS][4];
-#pragma unroll
-            for (int j = 0; j < kS; ++j)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) xb[j][q] = xa[j][q] ^ na[j];
-            const uint32_t Tb = Ta + gridDim.x;
-            if (Tb < ntiles) load_tile(p, Tb, wave, lane, xa, na);
-#pragma unroll
-            for (int j = 0; j < kS; ++j) {
-                const u32x4 v = {xb[j][0], xb[j][1], xb[j][2], xb[j][3]};
-                const uint32_t o = (uint32_t)(Ta % 16384u) * 32768u + (uint32_t)j * 16384u + wave * 1024u + 16u * lane;
-                __builtin_amdgcn_raw_buffer_store_b128(v, ro, (int)o, 0, 0);
-            }
-        }
-        return;
-    }
-#endif
-#if defined(BLT_EXP) && (BLT_EXP & 4096)
-    {   // timing experiment: phase 1 alone over static tiles (bytes prefetched one tile ahead)
-        uint32_t xa[kS][4], na[kS], xb[kS][4], nb[kS];
-        TileState st;
-        uint32_t acc = 0, it = 0;
-        uint32_t Ta = blockIdx.x;
-        if (Ta < ntiles) load_tile(p, Ta, wave, lane, xa, na);
-        for (; Ta < ntiles; Ta += 2 * gridDim.x) {
-            const uint32_t Tb = Ta + gridDim.x;
-#if BLT_EXP & 8192   // compute only: every tile reuses the first tile's bytes
-            if (Ta == blockIdx.x && Tb < ntiles) load_tile(p, Ta, wave, lane, xb, nb);
-#else
-            if (Tb < ntiles) load_tile(p, Tb, wave, lane, xb, nb);
-#endif
-            phase1_tile<kBE, kHiM>(tab, xa, na, tile_info(p, Ta), cs32, wave, lane, st, s_wfn[(it++) & 3]);
-            acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
-            if (Tb >= ntiles) break;
-            const uint32_t Tc = Tb + gridDim.x;
-#if !(BLT_EXP & 8192)
-            if (Tc < ntiles) load_tile(p, Tc, wave, lane, xa, na);
-#endif
-            phase1_tile<kBE, kHiM>(tab, xb, nb, tile_info(p, Tb), cs32, wave, lane, st, s_wfn[(it++) & 3]);
-            acc ^= st.v[0][0] ^ st.v[1][7] ^ st.ex[0] ^ st.ex[1] ^ st.mv[0] ^ st.lw[1];
-        }
-        if (acc == 0x9E3779B9u) p.ctl[15] = acc;
-        return;
-    }
-#endif
-    uint32_t T = uni(s_ticket[0]);    // tile in phase 1
-    uint32_t Tp = kNone;              // tile waiting for emission
-    uint32_t Tq = kNone;              // kTk2: the tile after T (kPf: its bytes are loaded during T's iteration)
-    if (kTk2) { Tq = uni(s_ticket[1]); if (T >= ntiles || Tq >= ntiles) Tq = kNone; }
-    __syncthreads();
-
-    uint32_t x[kS][4];      // input bytes of each sub-tile of T
-    uint32_t nxt[kS];       // byte after each wave range (lane 63's right neighbour)
-    uint32_t xq[kS][4];     // kPf: bytes of Tq
-    uint32_t nxtq[kS];
-    if (T < ntiles) load_tile(p, T, wave, lane, x, nxt);
+    uint32_t T = uni(s_tk[kRing - 2]);    // tile in phase 1
+    uint32_t Tp = kNone;                  // tile waiting for emission
+    uint32_t Tq = uni(s_tk[kRing - 1]);   // the tile after T (its bytes load during T's iteration)
+    if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     TInfo ti = {}, tip = {};
     if (T < ntiles) ti = tile_info(p, T);
-    TileState sp, sc;       // phase-1 state of Tp (pending) and of T (current)
-    uint64_t lbs[kLbWin];   // wave 0: status words for the pending tile's look-back
+    __syncthreads();
 
-    for (uint32_t it = 0; T < ntiles || Tp < ntiles; ++it) {
+    uint32_t xa[kS][4], xb[kS][4];   // input bytes of each sub-tile: T's, and Tq's (ping-pong)
+    uint32_t na[kS], nb[kS];         // byte after each wave range (lane 63's right neighbour)
+    if (T < ntiles) load_tile(p, T, wave, lane, xa, na);
+    TileState sa, sb;       // phase-1 states: T's and Tp's (ping-pong)
+    uint64_t lbs[kLbWin];   // look-back wave: status words for the pending tile's look-back
+    uint32_t it = 0;
+
+    // One iteration: phase 1 of T from `x` into `sc`, emission of Tp from `sp`, Tq's bytes into
+    // `xq`.  The loop runs it twice per trip with the roles swapped, so no state is copied.
+    auto step = [&](uint32_t (&x)[kS][4], uint32_t (&nxt)[kS], uint32_t (&xq)[kS][4], uint32_t (&nxtq)[kS],
+                    TileState& sc, const TileState& sp) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
         uint64_t stamp[7];
         const bool stamping = kTiming && p.debug != nullptr;
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-        if (kPf && Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
-        // the tile after T, claimed now and loaded after phase 1: claimed one phase before its
-        // bytes are needed, so claim order stays close to publish order (a tile claimed two
-        // iterations ahead lands behind later-claimed ones and stalls their look-backs)
+        if (Tq < ntiles) load_tile(p, Tq, wave, lane, xq, nxtq);   // a whole iteration to land
+        // the tile after Tq, claimed now: claimed one phase before its bytes are needed, so claim
+        // order stays close to publish order (a tile claimed further ahead lands behind
+        // later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
-#if defined(BLT_EXP) && (BLT_EXP & 256)
-        if (tid == 64 && (kTk2 ? Tq : T) < ntiles) tk = (kTk2 ? Tq : T) + gridDim.x;
-#else
-        if (tid == 64 && (kTk2 ? Tq : T) < ntiles) tk = atomicAdd(p.ctl, 1u);
-#endif
+        if (tid == 64 && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
         bool lbw = wave == 0;   // the wave that resolves Tp: the first to finish phase 1
         if (T < ntiles) {
-#if defined(BLT_EXP) && (BLT_EXP & 16)
-            if (T == kNone - 1u)   // timing experiment: no phase 1 (state left as it was)
-#endif
             // issue priority by age: the youngest waves lose the arbiter to the older ones, finish
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
@@ -1499,10 +1343,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
         }
-        if (!kTk2 && tid == 64) {
-            s_ticket[slot] = tk;
-            lds_release(&s_tkdone, it + 1u);
-        }
         if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
         // ---- carry-in and offset of Tp, by the first wave to finish phase 1: its snapshot is
@@ -1510,13 +1350,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (lbw && Tp < ntiles) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
             uint64_t O = 0ull;
-#if defined(BLT_EXP) && (BLT_EXP & 32768)
-            // timing experiment: no look-back (C, O of a dense text tile; wrong near chunk ends)
-            const bool lb = false;
-            O = (uint64_t)Tp * (kTilePosBytes / 2);
-#else
             const bool lb = Tp > 0;
-#endif
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
@@ -1558,23 +1392,11 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             }
         }
 
-        // ---- load Tn's bytes (after wave 0's look-back: its wait must not cover them); emit Tp
-        // T's bytes are consumed: the loads fly during the emission
-        uint32_t Tn = kNone;
-        if (!kTk2 && T < ntiles) {
-            wait_ge(p, &s_tkdone, it + 1u);
-            Tn = uni(s_ticket[slot]);
-            if (Tn >= ntiles) Tn = kNone;
-        }
-        if (kTk2 && !kPf) Tn = Tq;
-        if (!kPf && Tn < ntiles) load_tile(p, Tn, wave, lane, x, nxt);
+        // ---- emission of Tp (T's bytes are consumed; Tq's loads fly meanwhile) ----------------
         if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
             wait_ge(p, &s_lbdone, it + 1u);
             if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
-#if defined(BLT_EXP) && (BLT_EXP & 8)
-            if (Tp == kNone - 1u)   // timing experiment: no emission
-#endif
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
             const uint32_t Cp = uni(s_C[pslot]);
             if (Cp <= 1u)   // C = 2: a failed tile (flagged), no output
@@ -1592,35 +1414,30 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;
             e[2] = __builtin_amdgcn_s_memtime();
         }
-        if (kTk2) {
-            // Tq <- the ticket claimed at this iteration's start (handed over after the claiming
-            // wave's emission: a whole iteration for the atomic); kPf: T <- Tq's bytes, loaded then
-            if (tid == 64) {
-                s_ticket[slot] = tk;
-                lds_release(&s_tkdone, it + 1u);
-            }
-            uint32_t Tr = kNone;
-            if (Tq < ntiles) {
-                wait_ge(p, &s_tkdone, it + 1u);
-                Tr = uni(s_ticket[slot]);
-                if (Tr >= ntiles) Tr = kNone;
-                if (kPf) {
-#pragma unroll
-                    for (int j = 0; j < kS; ++j) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) x[j][q] = xq[j][q];
-                        nxt[j] = nxtq[j];
-                    }
-                }
-            }
-            Tn = Tq;
-            Tq = Tr;
+        // Tq <- the ticket claimed at this iteration's start (handed over after the claiming
+        // wave's emission); T <- Tq (its bytes were loaded during this iteration)
+        if (tid == 64) {
+            s_tk[slot] = tk;
+            lds_release(&s_tkdone, it + 1u);
         }
-        sp = sc;
+        uint32_t Tr = kNone;
+        if (Tq < ntiles) {
+            wait_ge(p, &s_tkdone, it + 1u);
+            Tr = uni(s_tk[slot]);
+            if (Tr >= ntiles) Tr = kNone;
+        }
         tip = ti;
-        if (Tn < ntiles) ti = tile_info(p, Tn);
+        if (Tq < ntiles) ti = tile_info(p, Tq);
         Tp = T;
-        T = Tn;
+        T = Tq;
+        Tq = Tr;
+        ++it;
+    };
+    for (;;) {
+        if (!(T < ntiles || Tp < ntiles)) break;
+        step(xa, na, xb, nb, sa, sb);
+        if (!(T < ntiles || Tp < ntiles)) break;
+        step(xb, nb, xa, na, sb, sa);
     }
 }
 

@@ -8,6 +8,6 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
 for v in "$@"; do
-  BLT_LIB_PATH=$R/build/exp/libblt_bpe_$v.so timeout -k 10 120 python tools/kbench.py --only "$ONLY" --tag "$v" >> "$O/kb.jsonl" 2>> "$O/kb.err"
+  BLT_LIB_PATH=$R/build/exp/libblt_bpe_$v.so timeout -k 10 180 python tools/kbench.py --only "$ONLY" --tag "$v" ${KB_ARGS:-} >> "$O/kb.jsonl" 2>> "$O/kb.err"
 done
 cat "$O/kb.jsonl"
