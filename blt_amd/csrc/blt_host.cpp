@@ -305,19 +305,19 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
         if (a < 256 && b < 256) h->dense[blt::dense_index(a, b)] = kv.second;
     }
     auto bswap = [](uint32_t v) { return (uint16_t)(((v & 0xFF) << 8) | ((v >> 8) & 0xFF)); };
-    h->self_ne.resize(65536);
+    h->self_ne.assign(blt::kSelfEntries, 0);
     for (uint32_t a = 0; a < 256; ++a)
-        for (uint32_t b = 0; b < 256; ++b) h->self_ne[blt::dense_index(a, b)] = (uint16_t)a;
+        for (uint32_t b = 0; b < 256; ++b) h->self_ne[blt::self_index(a, b)] = (uint16_t)a;
     for (const auto& kv : map) {
         const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
         if (a < 256 && b < 256) {
-            h->self_ne[blt::dense_index(a, b)] = kv.second;
+            h->self_ne[blt::self_index(a, b)] = kv.second;
             if (kv.second == a) h->self_ok = false;
             if (kv.second < 256) h->hi_merge = false;
         }
     }
-    h->self_be.resize(65536);
-    for (int i = 0; i < 65536; ++i) h->self_be[i] = bswap(h->self_ne[i]);
+    h->self_be.resize(blt::kSelfEntries);
+    for (uint32_t i = 0; i < blt::kSelfEntries; ++i) h->self_be[i] = bswap(h->self_ne[i]);
     if (!h->single_pass) {
         uint64_t cap = 16;
         while (cap < 2 * (uint64_t)map.size() + 2) cap <<= 1;
@@ -352,11 +352,11 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
                   hipMalloc(&t.dense, 65536 * sizeof(uint16_t)) == hipSuccess &&
                   hipMemcpyAsync(t.dense, h->dense.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice, us) ==
                       hipSuccess &&
-                  hipMalloc(&t.self_ne, 65536 * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.self_ne, h->self_ne.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                  hipMalloc(&t.self_ne, blt::kSelfEntries * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.self_ne, h->self_ne.data(), blt::kSelfEntries * sizeof(uint16_t), hipMemcpyHostToDevice,
                                  us) == hipSuccess &&
-                  hipMalloc(&t.self_be, 65536 * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.self_be, h->self_be.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice,
+                  hipMalloc(&t.self_be, blt::kSelfEntries * sizeof(uint16_t)) == hipSuccess &&
+                  hipMemcpyAsync(t.self_be, h->self_be.data(), blt::kSelfEntries * sizeof(uint16_t), hipMemcpyHostToDevice,
                                  us) == hipSuccess;
         if (ok && !h->hslots.empty()) {
             const size_t bytes = h->hslots.size() * sizeof(uint64_t);

@@ -55,6 +55,14 @@ hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStrea
 // Dense-table layout shared with the host: entry for byte pair (a, b).
 inline uint32_t dense_index(uint32_t a, uint32_t b) { return (a << 8) | (b ^ ((a << 1) & 0xFEu)); }
 
+// Self-token table of the byte pass: rows of kSelfRow u16 entries (256 used), entry (a, b) at
+// a * kSelfRow + b.  The 2-entry pad per row skews rows across the LDS banks: the dword of (a, b)
+// is 129 a + b / 2, its bank (a + b / 2) mod 32, so lanes reading pairs with the same second byte
+// (English text) spread over the banks; the byte address 516 a + 2 b + base is one v_dot2_u32_u16.
+constexpr uint32_t kSelfRow = 258;
+constexpr uint32_t kSelfEntries = 256 * kSelfRow;
+inline uint32_t self_index(uint32_t a, uint32_t b) { return a * kSelfRow + b; }
+
 // Hash used by the general-map slots (must match hash_get in bpe_kernels.hip).
 inline uint64_t slot_hash(uint32_t key) {
     uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;

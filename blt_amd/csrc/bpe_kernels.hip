@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "bpe_kernels.h"
 
 namespace blt {
@@ -705,18 +707,24 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         // right neighbour of position 15: next lane's first byte (wave_shl:1); lane 63 keeps
-        // the "old" operand, the byte after the wave's range
-        const uint32_t nb =
-            (uint32_t)__builtin_amdgcn_update_dpp((int)nxt[j], (int)x[j][0], 0x130, 0xF, 0xF, false) & 0xFFu;
-        uint32_t t0[8];
+        // the "old" operand, the byte after the wave's range (byte 0 of nbw; bytes 1..3 unused)
+        const uint32_t nbw = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt[j], (int)x[j][0], 0x130, 0xF, 0xF, false);
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-            // (k, k+1) = (2h, 2h+1): 16-bit halves (x[k] << 8 | x[k+1]), (x[k+1] << 8 | x[k+2])
-            const uint32_t lo = x[j][h >> 1], hi = (h >> 1) < 3 ? x[j][(h >> 1) + 1] : nb;
-            t0[h] = __builtin_amdgcn_perm(hi, lo, (h & 1) ? 0x03040203u : 0x01020001u);
-            const uint32_t t = t0[h] ^ ((t0[h] >> 7) & 0x00FE00FEu);      // bank swizzle of b
-            const uint32_t va = *(const lds_u16*)(uintptr_t)tab_addr_lo(t, tab);
-            const uint32_t vb = *(const lds_u16*)(uintptr_t)tab_addr_hi(t, tab);
+            uint32_t va, vb;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                // position k = 2h + e: bytes (x_k, x_k+1) as u16 lanes [x_k, x_k+1] (one perm), then
+                // the entry's LDS byte address 516 x_k + 2 x_k+1 + tab (one dot2, kSelfRow layout)
+                const int k = 2 * h + e;
+                const uint32_t lo = x[j][k >> 2], hi = (k >> 2) < 3 ? x[j][(k >> 2) + 1] : nbw;
+                const uint32_t sel = 0x0C000C00u | ((uint32_t)((k & 3) + 1) << 16) | (uint32_t)(k & 3);
+                const uint32_t pr = __builtin_amdgcn_perm(hi, lo, sel);
+                const uint32_t addr = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, pr),
+                                                             (u16x2){(unsigned short)(2 * kSelfRow), 2}, tab, false);
+                const uint32_t v = *(const lds_u16*)(uintptr_t)addr;
+                if (e == 0) va = v; else vb = v;
+            }
             st.v[j][h] = __builtin_amdgcn_perm(vb, va, 0x05040100u);   // va | vb << 16, one op
         }
         uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
@@ -727,8 +735,11 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
                 // a merge is a token >= 256, a itself < 256: the token's high byte (BE: low byte)
                 d = st.v[j][h] & (kBE ? 0x00FF00FFu : 0xFF00FF00u);
             } else {
-                // token of a itself, in output byte order: BE (a << 8), native a
-                const uint32_t self = kBE ? (t0[h] & 0xFF00FF00u) : ((t0[h] >> 8) & 0x00FF00FFu);
+                // token of a itself (positions 2h, 2h+1: bytes 2h, 2h+1 of the lane), in output
+                // byte order: BE (a << 8), native a
+                const uint32_t xw = x[j][h >> 1];
+                const uint32_t self = kBE ? __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x030C020Cu : 0x010C000Cu)
+                                          : __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x0C030C02u : 0x0C010C00u);
                 d = st.v[j][h] ^ self;
             }
             m32 |= pk_nz(d) << (2 * h);
@@ -1256,7 +1267,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
 // with the ticket delays the hand-over, and cfg3 loses 2 %.)
 template <bool kBE, bool kHiM>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];
+    __shared__ __attribute__((aligned(16))) uint16_t s_tab[kSelfEntries];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
     __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroups][4];   // wave functions (phase 1)
     __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
@@ -1286,7 +1297,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
-        for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
+        for (int i = tid; i < (int)(kSelfEntries * 2 / 16); i += kThreads) dst[i] = src[i];
     }
     __syncthreads();
     const uint32_t tab = uni(lds_addr(s_tab));
@@ -1525,17 +1536,27 @@ __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
 }
 
 // ---- launchers ---------------------------------------------------------------------------
-static int grid_for_tiles(uint32_t ntiles, int device, const void* fn) {
-    static int cached_cus[64] = {0};
-    static int cached_occ[64][4] = {{0}};
-    (void)cached_occ;
-    int cus = device < 64 ? cached_cus[device] : 0;
-    if (!cus) {
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (device < 64) cached_cus[device] = cus;
+// Persistent-grid size of a kernel on a device: CUs x resident workgroups per CU, queried once
+// per (device, kernel) and cached in atomics (launchers run concurrently from many host threads).
+struct GridCache {
+    std::atomic<int> cus[64];
+    std::atomic<int> occ[64][6];
+};
+static GridCache g_grid;   // zero-initialised (static storage)
+static int grid_for(uint32_t ntiles, int device, const void* fn, int threads, int kernel_id) {
+    int cus = 0, occ = 0;
+    if (device >= 0 && device < 64) {
+        cus = g_grid.cus[device].load(std::memory_order_relaxed);
+        occ = g_grid.occ[device][kernel_id].load(std::memory_order_relaxed);
     }
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kThreads, 0) != hipSuccess || occ < 1) occ = 1;
+    if (!cus) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 1;
+        if (device >= 0 && device < 64) g_grid.cus[device].store(cus, std::memory_order_relaxed);
+    }
+    if (!occ) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, 0) != hipSuccess || occ < 1) occ = 1;
+        if (device >= 0 && device < 64) g_grid.occ[device][kernel_id].store(occ, std::memory_order_relaxed);
+    }
     long long g = (long long)cus * occ;
     if (g > (long long)ntiles) g = ntiles;
     return (int)(g < 1 ? 1 : g);
@@ -1546,7 +1567,7 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
     const void* fn;
     if (!input_u16) fn = big_endian ? (const void*)merge_pass_kernel<uint8_t, true> : (const void*)merge_pass_kernel<uint8_t, false>;
     else fn = big_endian ? (const void*)merge_pass_kernel<uint16_t, true> : (const void*)merge_pass_kernel<uint16_t, false>;
-    const int grid = grid_for_tiles(p.ntiles, device, fn);
+    const int grid = grid_for(p.ntiles, device, fn, kThreads, (input_u16 ? 2 : 0) + (big_endian ? 1 : 0));
     if (!input_u16) {
         if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint8_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
         else hipLaunchKernelGGL((merge_pass_kernel<uint8_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
@@ -1563,12 +1584,8 @@ hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, 
                                             : (const void*)seg::scan_bytes_kernel<true, false>)
                                 : (hi_merge ? (const void*)seg::scan_bytes_kernel<false, true>
                                             : (const void*)seg::scan_bytes_kernel<false, false>);
-    int cus = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, seg::kThreads, 0) != hipSuccess || occ < 1) occ = 1;
-    long long grid = (long long)(cus > 0 ? cus : 1) * occ;
-    if (grid > (long long)p.ntiles) grid = p.ntiles;
+    // every byte-pass instantiation holds the whole LDS: one workgroup per CU, one cache entry
+    const int grid = grid_for(p.ntiles, device, fn, seg::kThreads, 4);
     const dim3 g((unsigned)grid), b(seg::kThreads);
     if (big_endian) {
         if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<true, true>), g, b, 0, s, p);
