@@ -39,6 +39,13 @@ def main():
             host, merges = synth.text(n, seed=3), m3
         elif cfg == "cfg5":
             host, merges = synth.random_bytes(n, seed=5), m3
+        elif cfg.startswith("text"):   # textN: N MiB of cfg2's text with cfg2's merges (size sweeps)
+            mib = int(cfg[4:])
+            host = synth.text(mib << 20, seed=2)
+            merges = synth.merges_dict(synth.top_pair_merges(synth.text(100 << 20, seed=2), 256))
+        elif cfg == "cfg2big":   # cfg2's text and merges at the --mib size: steady-state cost per tile
+            host = synth.text(n, seed=2)
+            merges = synth.merges_dict(synth.top_pair_merges(host[: 100 << 20], 256))
         else:
             raise SystemExit(f"unknown config {cfg}")
         s = blt_amd.BpeStrategy(merges)
