@@ -238,7 +238,7 @@ struct DevTables {
     uint16_t* dense = nullptr;      // native u16 values, sentinel where absent (general kernel)
     uint16_t* self_ne = nullptr;    // self-token table, native byte order (byte-pass kernel)
     uint16_t* self_be = nullptr;    // self-token table, output (big-endian) byte order
-    uint64_t* hslots = nullptr;
+    uint4* hbuckets = nullptr;      // general map: cuckoo buckets (u16 passes)
 };
 
 struct blt_bpe {
@@ -253,8 +253,10 @@ struct blt_bpe {
     // kernel then reads "merge" off the entry's high byte instead of comparing it with a.
     bool hi_merge = true;
     std::vector<uint16_t> self_ne, self_be;
-    std::vector<uint64_t> hslots;          // general map, empty when single_pass
-    uint64_t hmask = 0;
+    // General map (not single_pass): 2-choice cuckoo table of buckets of two slots for the u16
+    // passes (blt::bucket_of), words [key0, val0, key1, val1]; val = BE(value) | 1 << 16.
+    std::vector<uint32_t> hwords;
+    uint32_t hmul1 = 0, hmul2 = 0, hshift = 0;
     DevTables dev[kMaxDevices];
     // Sticky device-error word in pinned, mapped host memory: any kernel of this handle that flags
     // an error (look-back timeout, output range, prefix invariant) stores 1 here, and every later
@@ -265,6 +267,59 @@ struct blt_bpe {
 };
 
 namespace {
+
+// 2-choice cuckoo placement of the general map (u16 passes): buckets of two slots, load at most
+// one half, multiplicative hashes; new multipliers (and then twice the buckets) until every key
+// has a place.  Empty slots hold a key that is not in the map.
+bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, blt_bpe* h) {
+    uint32_t empty = 0xFFFFFFFFu;
+    while (map.count(empty)) --empty;
+    uint32_t log2nb = 2;
+    while ((1u << log2nb) < map.size()) ++log2nb;
+    uint64_t seed = 0x9E3779B97F4A7C15ull;
+    auto next_mul = [&seed]() {
+        seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint32_t)(seed >> 32) | 1u;
+    };
+    for (; log2nb <= 24; ++log2nb) {
+        const uint32_t nb = 1u << log2nb, shift = 32 - log2nb;
+        for (int attempt = 0; attempt < 32; ++attempt) {
+            const uint32_t m1 = next_mul(), m2 = next_mul();
+            std::vector<uint32_t> key(2ull * nb, empty), val(2ull * nb, 0);
+            bool ok = true;
+            for (const auto& kv : map) {
+                uint32_t k = kv.first, v = ((uint32_t)((kv.second & 0xFF) << 8) | (kv.second >> 8)) | 0x10000u;
+                uint32_t b = blt::bucket_of(k, m1, shift);
+                bool placed = false;
+                for (int kick = 0; kick < 512 && !placed; ++kick) {
+                    const uint32_t b2 = blt::bucket_of(k, m2, shift);
+                    for (uint32_t c : {b, b2})
+                        for (int sl = 0; sl < 2 && !placed; ++sl)
+                            if (key[2 * c + sl] == empty) { key[2 * c + sl] = k; val[2 * c + sl] = v; placed = true; }
+                    if (placed) break;
+                    // evict a slot of b (alternating), carry the evicted key to its other bucket
+                    const uint32_t sl = kick & 1u;
+                    std::swap(k, key[2 * b + sl]);
+                    std::swap(v, val[2 * b + sl]);
+                    const uint32_t o1 = blt::bucket_of(k, m1, shift), o2 = blt::bucket_of(k, m2, shift);
+                    b = (o1 == b) ? o2 : o1;
+                }
+                if (!placed) { ok = false; break; }
+            }
+            if (!ok) continue;
+            h->hwords.assign(4ull * nb, 0);
+            for (uint32_t i = 0; i < 2 * nb; ++i) {
+                h->hwords[2 * i] = key[i];
+                h->hwords[2 * i + 1] = val[i];
+            }
+            h->hmul1 = m1;
+            h->hmul2 = m2;
+            h->hshift = shift;
+            return true;
+        }
+    }
+    return false;
+}
 
 int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>& vals, blt_bpe** out) {
     std::unique_ptr<blt_bpe> h(new (std::nothrow) blt_bpe());
@@ -318,17 +373,7 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
     }
     h->self_be.resize(blt::kSelfEntries);
     for (uint32_t i = 0; i < blt::kSelfEntries; ++i) h->self_be[i] = bswap(h->self_ne[i]);
-    if (!h->single_pass) {
-        uint64_t cap = 16;
-        while (cap < 2 * (uint64_t)map.size() + 2) cap <<= 1;
-        h->hslots.assign(cap, 0);
-        h->hmask = cap - 1;
-        for (const auto& kv : map) {
-            uint64_t s = blt::slot_hash(kv.first) & h->hmask;
-            while (h->hslots[s] >> 63) s = (s + 1) & h->hmask;
-            h->hslots[s] = (1ull << 63) | ((uint64_t)kv.second << 32) | kv.first;
-        }
-    }
+    if (!h->single_pass && !build_buckets(map, h.get())) return fail(BLT_E_NOMEM, "cannot place the merge map in a hash table");
     *out = h.release();
     return 0;
 }
@@ -358,10 +403,10 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
                   hipMalloc(&t.self_be, blt::kSelfEntries * sizeof(uint16_t)) == hipSuccess &&
                   hipMemcpyAsync(t.self_be, h->self_be.data(), blt::kSelfEntries * sizeof(uint16_t), hipMemcpyHostToDevice,
                                  us) == hipSuccess;
-        if (ok && !h->hslots.empty()) {
-            const size_t bytes = h->hslots.size() * sizeof(uint64_t);
-            ok = hipMalloc(&t.hslots, bytes) == hipSuccess &&
-                 hipMemcpyAsync(t.hslots, h->hslots.data(), bytes, hipMemcpyHostToDevice, us) == hipSuccess;
+        if (ok && !h->hwords.empty()) {
+            const size_t bytes = h->hwords.size() * sizeof(uint32_t);
+            ok = hipMalloc(&t.hbuckets, bytes) == hipSuccess &&
+                 hipMemcpyAsync(t.hbuckets, h->hwords.data(), bytes, hipMemcpyHostToDevice, us) == hipSuccess;
         }
         ok = ok && hipStreamSynchronize(us) == hipSuccess;
         if (us) (void)hipStreamDestroy(us);
@@ -409,23 +454,19 @@ struct WsLayout {
 
 WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     WsLayout L{};
-    const uint64_t tile = std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes);
+    const uint64_t tile = single_pass ? std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes) : blt::kTilePosU16;
     L.ntiles = (n + tile - 1) / tile;
     L.nchunks = n ? (n + cs - 1) / cs : 0;
     L.ctl = 0;
     L.status = blt::kCtlBytes;
     L.zero_bytes = up16(blt::kCtlBytes + 8 * L.ntiles);
-    L.total = L.zero_bytes;
-    L.off_a = L.total + 16;
+    L.total = L.zero_bytes;   // u64 [2] pass totals (alternating), u32 done flag, pad: 32 bytes
+    L.off_a = L.total + 32;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.tok_a = L.off_b + up16(8 * (L.nchunks + 1));
-    if (single_pass) {
-        L.tok_b = L.tok_a;
-        L.bytes = L.tok_a;
-    } else {
-        L.tok_b = L.tok_a + up16(2 * n);
-        L.bytes = L.tok_b + up16(2 * n);
-    }
+    L.tok_b = L.tok_a;
+    // a general map's passes alternate between the caller's output and one workspace buffer
+    L.bytes = single_pass ? L.tok_a : L.tok_a + up16(2 * n);
     return L;
 }
 
@@ -453,11 +494,18 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
 }
 
 // Enqueues one merge pass over n positions.
+// u16 passes of a general map: the token count comes from the device and is written there.
+struct Chain {
+    const uint64_t* n_in = nullptr;   // count written by the previous pass
+    uint64_t* n_out = nullptr;        // this pass's count
+    uint32_t* done = nullptr;         // set by a pass that merged nothing
+};
+
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
-             uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false) {
+             uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr) {
     const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->self_ok;   // byte-pass fast kernel
-    const uint64_t tile = columnar ? blt::kTilePosBytes : blt::kTilePos;
+    const uint64_t tile = columnar ? blt::kTilePosBytes : in_u16 ? blt::kTilePosU16 : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
     if (!ws_zeroed) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
@@ -472,12 +520,19 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.chunk_off = chunk_off;
     p.status = reinterpret_cast<uint64_t*>(ws + L.status);
     p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
-    p.total = reinterpret_cast<uint64_t*>(ws + L.total);
+    p.total = chain ? chain->n_out : reinterpret_cast<uint64_t*>(ws + L.total);
+    if (chain) {
+        p.n_dev = chain->n_in;
+        p.done = chain->done;
+    }
     p.ntiles = (uint32_t)ntiles;
     p.sentinel = h->sentinel;
     p.dense = columnar ? (be ? t->self_be : t->self_ne) : t->dense;
-    p.hslots = t->hslots;
-    p.hmask = h->hmask;
+    p.hbuckets = t->hbuckets;
+    p.hmul1 = h->hmul1;
+    p.hmul2 = h->hmul2;
+    p.hshift = h->hshift;
+    p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
     p.cs_magic = cs ? ~0ull / cs : 0;
     if (cs && cs % blt::kTilePosBytes == 0 && cs / blt::kTilePosBytes < (1ull << 31)) {
         p.cs_tiles = (uint32_t)(cs / blt::kTilePosBytes);
@@ -523,35 +578,40 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         return 0;
     }
 
-    // General map: pass 1 on bytes, then passes on u16 tokens until one merges nothing
-    // (tokenizer.rs:63-86), then big-endian serialisation (:88-91).
-    uint16_t* tok[2] = {reinterpret_cast<uint16_t*>(ws + L.tok_a), reinterpret_cast<uint16_t*>(ws + L.tok_b)};
-    uint64_t* off[2] = {reinterpret_cast<uint64_t*>(ws + L.off_a), reinterpret_cast<uint64_t*>(ws + L.off_b)};
-    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, tok[0], false, 2 * n, off[0])) return rc;
-    uint64_t cur_n;
-    if (int rc = read_u64(ws + L.total, &cur_n, s)) return rc;
-    if (int rc = check_ctl(ws, s)) return rc;
+    // General map: pass 1 on bytes, then passes on big-endian u16 tokens until one merges
+    // nothing (tokenizer.rs:63-86; a pass that merges nothing leaves the tokens, so running it
+    // for every chunk once the slowest chunk is done changes nothing).  Passes alternate between
+    // d_out and one workspace buffer; the pass that merges nothing writes its input unchanged, so
+    // both then hold the result.  The host enqueues kBatch passes at a time and reads the pass
+    // totals and the done flag once per batch (passes after the done one return at once).
+    constexpr int kBatch = 4;
+    uint8_t* tok[2] = {d_out, ws + L.tok_a};
+    uint64_t* off[2] = {d_chunk_off ? d_chunk_off : reinterpret_cast<uint64_t*>(ws + L.off_a),
+                        reinterpret_cast<uint64_t*>(ws + L.off_b)};
+    uint64_t* tot = reinterpret_cast<uint64_t*>(ws + L.total);
+    uint32_t* done = reinterpret_cast<uint32_t*>(ws + L.total + 16);
+    HIP_TRY(hipMemsetAsync(tot, 0, 32, s));
+    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, tok[0], true, 2 * n, off[0])) return rc;
     int cur = 0;
-    if (cur_n != n) {
-        for (;;) {
-            const int nx = cur ^ 1;
-            if (int rc = run_pass(h, t, dev, s, ws, L, tok[cur], true, cur_n, 0, off[cur], tok[nx], false, 2 * n, off[nx]))
+    uint64_t k = 1;   // u16 passes enqueued
+    uint64_t rec[4] = {0, 0, 0, 0};
+    for (;;) {
+        for (int b = 0; b < kBatch; ++b, ++k) {
+            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done};
+            if (int rc = run_pass(h, t, dev, s, ws, L, tok[cur], true, n, 0, off[cur], tok[cur ^ 1], true, 2 * n,
+                                  off[cur ^ 1], false, &c))
                 return rc;
-            uint64_t nn;
-            if (int rc = read_u64(ws + L.total, &nn, s)) return rc;
-            if (int rc = check_ctl(ws, s)) return rc;
-            if (nn == cur_n) break;  // no merge: output == input
-            cur = nx;
-            cur_n = nn;
+            cur ^= 1;
         }
-    }
-    HIP_TRY(blt::launch_bswap16(tok[cur], cur_n, d_out, s));
-    if (d_chunk_off)
-        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
-    if (out_tokens) {
+        HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        *out_tokens = cur_n;
+        if (int rc = sticky_check(h)) return rc;
+        if ((uint32_t)rec[2]) break;
+        if (k > n + kBatch) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
+    if (d_chunk_off && off[0] != d_chunk_off)
+        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[0], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+    if (out_tokens) *out_tokens = rec[0];
     return 0;
 }
 
@@ -983,7 +1043,7 @@ void blt_bpe_destroy(blt_bpe* h) {
         if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);
         if (h->dev[d].self_ne) (void)hipFree(h->dev[d].self_ne);
         if (h->dev[d].self_be) (void)hipFree(h->dev[d].self_be);
-        if (h->dev[d].hslots) (void)hipFree(h->dev[d].hslots);
+        if (h->dev[d].hbuckets) (void)hipFree(h->dev[d].hbuckets);
     }
     if (h->sticky) (void)hipHostFree(h->sticky);
     delete h;

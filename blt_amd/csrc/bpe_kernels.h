@@ -7,6 +7,7 @@ namespace blt {
 
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
+constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the u16 passes
 constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
@@ -29,8 +30,14 @@ struct PassParams {
     const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout).  General
                                // kernel: native values, sentinel where absent.  Byte-pass kernel:
                                // self-token table (absent (a, b) -> a) in the output byte order
-    const uint64_t* hslots;    // general map: open-addressing slots (bit 63 used | v << 32 | key)
-    uint64_t hmask;
+    const uint4* hbuckets;     // general map (u16 passes): 2-choice cuckoo buckets of two slots,
+                               // [key0, val0, key1, val1]; key = a << 16 | b, val = BE(v) | 1 << 16,
+                               // empty slots hold hempty (a key not in the map) and val 0
+    uint32_t hmul1, hmul2;     // bucket of key: (key * hmul) >> hshift, two choices
+    uint32_t hshift;
+    uint32_t hbytes;           // table bytes (u16 passes stage the table in LDS when it fits)
+    const uint64_t* n_dev;     // u16 passes: the token count written by the previous pass (on device)
+    uint32_t* done;            // u16 passes: set when a pass merged nothing; later passes return at once
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
     uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles
                                // (below 2^31), else 0
@@ -42,6 +49,8 @@ struct PassParams {
                                // the iteration start, after the first and second barrier; spins
 };
 
+// Generic pass: byte input with the dense LDS table (maps the byte pass cannot take), or BE u16
+// tokens with the bucket table (p.hbuckets) for the later passes of a general map; output BE.
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);
 // Byte-input pass (segment kernel, seg::scan_bytes_kernel): p.cs >= kMinChunkBytes; tiles of
 // kTilePosBytes positions.
@@ -50,7 +59,6 @@ hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, 
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 // Test hook: runs the kernels' error path once (ctl nullable, sticky the handle's error word).
 hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s);
-hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 
 // Dense-table layout shared with the host: entry for byte pair (a, b).
 inline uint32_t dense_index(uint32_t a, uint32_t b) { return (a << 8) | (b ^ ((a << 1) & 0xFEu)); }
@@ -63,10 +71,9 @@ constexpr uint32_t kSelfRow = 258;
 constexpr uint32_t kSelfEntries = 256 * kSelfRow;
 inline uint32_t self_index(uint32_t a, uint32_t b) { return a * kSelfRow + b; }
 
-// Hash used by the general-map slots (must match hash_get in bpe_kernels.hip).
-inline uint64_t slot_hash(uint32_t key) {
-    uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
-    return h ^ (h >> 29);
-}
+// Bucket of a general-map key (must match bucket_get in bpe_kernels.hip).
+inline uint32_t bucket_of(uint32_t key, uint32_t mul, uint32_t shift) { return (uint32_t)(key * mul) >> shift; }
+// Largest general-map table staged in LDS (bytes); larger tables are read from global memory (L2).
+constexpr uint32_t kHashLdsMax = 48u << 10;
 
 }  // namespace blt

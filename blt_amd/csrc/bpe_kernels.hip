@@ -42,7 +42,6 @@ constexpr int kThreads = 512;                 // 8 waves; 1 workgroup per CU (LD
 constexpr int kWaves = kThreads / 64;
 constexpr int kSeg = 16;                      // positions per lane per sub-tile
 constexpr int kSubPos = kThreads * kSeg;      // 8192 positions per sub-tile
-constexpr int kGroups = kSub * kWaves;        // (sub-tile, wave) groups per tile
 constexpr int kStageBytes = 2 * kSubPos + 32;
 constexpr uint32_t kSpinLimit = 1u << 20;
 static_assert(kTilePos == kSub * kSubPos, "tile geometry");
@@ -275,30 +274,37 @@ template <> struct Seg<uint16_t> {
     static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
 };
 
-__device__ __forceinline__ bool hash_get(const PassParams& p, uint32_t a, uint32_t b, uint32_t& v) {
-    uint32_t key = (a << 16) | b;
-    uint64_t h = (uint64_t)key * 0x9E3779B97F4A7C15ull;
-    h = (h ^ (h >> 29)) & p.hmask;
-    for (;;) {
-        uint64_t s = p.hslots[h];
-        if (!(s >> 63)) return false;
-        if ((uint32_t)s == key) { v = (uint32_t)(s >> 32) & 0xFFFFu; return true; }
-        h = (h + 1) & p.hmask;
-    }
+// General-map lookup of key a << 16 | b: both candidate buckets are read (no probe loop), a
+// matching slot contributes its value word; found = bit 16, the value is stored big-endian.
+template <typename TabPtr>
+__device__ __forceinline__ bool bucket_get(const PassParams& p, TabPtr tab, uint32_t key, uint32_t& vbe) {
+    const uint4 x = tab[(key * p.hmul1) >> p.hshift];
+    const uint4 y = tab[(key * p.hmul2) >> p.hshift];
+    const uint32_t r = (x.x == key ? x.y : 0u) | (x.z == key ? x.w : 0u) | (y.x == key ? y.y : 0u) |
+                       (y.z == key ? y.w : 0u);
+    vbe = r & 0xFFFFu;
+    return (r >> 16) != 0u;
 }
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t t) { return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu); }
 
-// One merge pass over the whole buffer.  InT = uint8_t: byte input, dense LDS table.
-// InT = uint16_t: token input, global hash table.  kBE: write big-endian u16 (final output),
-// else native u16 tokens for the next pass.
-template <typename InT, bool kBE>
-__global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
+// One merge pass over the whole buffer.  InT = uint8_t: byte input, dense LDS table (maps the
+// byte pass cannot take).  InT = uint16_t: big-endian token input (the previous pass's output),
+// the bucket table in LDS (kHashLds, dynamic shared memory) or global memory; the token count
+// comes from the device (p.n_dev) and a pass after one that merged nothing returns at once, so
+// the host enqueues passes without waiting for their counts.  kBE: write big-endian u16, else
+// native u16.
+template <typename InT, bool kBE, bool kHashLds>
+__device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     constexpr bool kDense = sizeof(InT) == 1;
+    constexpr int kSubT = kSub;
+    constexpr uint64_t kTileT = (uint64_t)kSubT * kSubPos;
+    constexpr int kGroupsT = kSubT * kWaves;
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[kDense ? 65536 : 8];
+    extern __shared__ uint4 s_hash[];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kStageBytes];
-    __shared__ WaveFn s_wfn[kGroups];
-    __shared__ uint32_t s_gin[kGroups][4];   // carry-in (H=0, H=1), offset (H=0, H=1)
+    __shared__ WaveFn s_wfn[kGroupsT];
+    __shared__ uint32_t s_gin[kGroupsT][4];   // carry-in (H=0, H=1), offset (H=0, H=1)
     __shared__ uint32_t s_tfn[4];            // tile function: co0, co1, cnt0, cnt1
     __shared__ uint32_t s_ticket;
     __shared__ uint32_t s_C;
@@ -307,6 +313,14 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    PassParams p = pin;
+    if constexpr (!kDense) {
+        if (p.done && __hip_atomic_load(p.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+        if (p.n_dev) {
+            p.n = __hip_atomic_load(const_cast<uint64_t*>(p.n_dev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            p.ntiles = (uint32_t)((p.n + kTileT - 1) / kTileT);
+        }
+    }
     const InT* in = reinterpret_cast<const InT*>(p.in);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
 
@@ -314,6 +328,8 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
         for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
+    } else if constexpr (kHashLds) {
+        for (uint32_t i = tid; i < p.hbytes / 16u; i += kThreads) s_hash[i] = p.hbuckets[i];
     }
 
     for (;;) {
@@ -321,15 +337,15 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
         __syncthreads();
         const uint32_t T = s_ticket;
         if (T >= p.ntiles) break;
-        const uint64_t tile0 = (uint64_t)T * kTilePos;
+        const uint64_t tile0 = (uint64_t)T * kTileT;
 
-        Seg<InT> seg[kSub];
-        uint32_t vals[kSub][8];
-        uint32_t mm[kSub], valid[kSub], hasb[kSub], bco[kSub], excl[kSub];
+        Seg<InT> seg[kSubT];
+        uint32_t vals[kSubT][8];
+        uint32_t mm[kSubT], valid[kSubT], hasb[kSubT], bco[kSubT], excl[kSubT];
 
         // ---- phase 1: lookups and per-lane / per-wave carry functions --------------------
 #pragma unroll
-        for (int j = 0; j < kSub; ++j) {
+        for (int j = 0; j < kSubT; ++j) {
             const uint64_t sub0 = tile0 + (uint64_t)j * kSubPos;
             const uint64_t pos = sub0 + (uint64_t)tid * kSeg;
             seg[j].load(in, pos, p.n);
@@ -346,7 +362,11 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
                     v = s_tab[swz_index(a, b)];
                     hit = (p.sentinel > 0xFFFFu) || (v != p.sentinel);
                 } else {
-                    hit = hash_get(p, a, b, v);
+                    // tokens are big-endian in memory; the key is native (a << 16 | b), the value
+                    // comes back big-endian
+                    const uint32_t key = (bswap16(a) << 16) | bswap16(b);
+                    if constexpr (kHashLds) hit = bucket_get(p, (const uint4*)s_hash, key, v);
+                    else hit = bucket_get(p, p.hbuckets, key, v);
                 }
                 m |= (uint32_t)hit << k;
                 if (k & 1) vals[j][k >> 1] |= v << 16; else vals[j][k >> 1] = v;
@@ -381,13 +401,13 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
         // ---- phase 2: tile function, publish, look-back ----------------------------------
         if (wave == 0) {
             uint32_t gi = 0, gco = 0, g0 = 0, g1 = 0;
-            if (lane < kGroups) { WaveFn f = s_wfn[lane]; gi = f.ident; gco = f.cout; g0 = f.cnt0; g1 = f.cnt1; }
+            if (lane < kGroupsT) { WaveFn f = s_wfn[lane]; gi = f.ident; gco = f.cout; g0 = f.cnt0; g1 = f.cnt1; }
             else { gi = 1; }
             uint32_t ghb, gbc, gex;
             WaveFn tf;
             // group counts fit 16 bits each (<= 1024 per group, <= 32768 per tile)
             resolve_wave(gi, gco, g0, g1, lane, ghb, gbc, gex, tf);
-            if (lane < kGroups) {
+            if (lane < kGroupsT) {
                 s_gin[lane][0] = ghb ? gbc : 0u;
                 s_gin[lane][1] = ghb ? gbc : 1u;
                 s_gin[lane][2] = gex & 0xFFFFu;
@@ -423,6 +443,7 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
                 if (T == p.ntiles - 1) {
                     *p.total = end;
                     if (p.chunk_off) p.chunk_off[p.nchunks] = end;
+                    if (!kDense && p.done && end == p.n) *p.done = 1u;   // no merge: the fixpoint
                 }
             }
         }
@@ -434,7 +455,7 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
         const uint64_t O = s_O;
         const uint32_t tile_cnt = C ? s_tfn[3] : s_tfn[2];
 #pragma unroll
-        for (int j = 0; j < kSub; ++j) {
+        for (int j = 0; j < kSubT; ++j) {
             const uint64_t sub0 = tile0 + (uint64_t)j * kSubPos;
             const uint64_t pos = sub0 + (uint64_t)tid * kSeg;
             const int g = j * kWaves + wave;
@@ -443,7 +464,7 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
             const uint32_t c = hasb[j] ? bco[j] : cg;
             const uint32_t lane_off = og + (cg ? (excl[j] >> 16) : (excl[j] & 0xFFFFu));
             const uint32_t sub_first = s_gin[j * kWaves][2 + C];
-            const uint32_t sub_end = (j + 1 < kSub) ? s_gin[(j + 1) * kWaves][2 + C] : tile_cnt;
+            const uint32_t sub_end = (j + 1 < kSubT) ? s_gin[(j + 1) * kWaves][2 + C] : tile_cnt;
             const uint64_t gb = 2ull * (O + sub_first), ge = 2ull * (O + sub_end);
             const uint64_t ab = gb & ~15ull;
             const uint32_t M = merges_for(mm[j], c);
@@ -454,8 +475,12 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
             for (int k = 0; k < 16; ++k) {
                 if ((L >> k) & 1u) {
                     uint32_t v = (vals[j][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                    uint32_t tok = ((M >> k) & 1u) ? v : seg[j].at(k);
-                    st16[r++] = (uint16_t)(kBE ? bswap16(tok) : tok);
+                    if constexpr (kDense) {
+                        const uint32_t tok = ((M >> k) & 1u) ? v : seg[j].at(k);
+                        st16[r++] = (uint16_t)(kBE ? bswap16(tok) : tok);
+                    } else {   // u16 input and table values are already big-endian
+                        st16[r++] = (uint16_t)(((M >> k) & 1u) ? v : seg[j].at(k));
+                    }
                 }
             }
             // token offsets of chunk starts in this segment
@@ -493,6 +518,17 @@ __global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
             __syncthreads();
         }
     }
+}
+
+template <typename InT, bool kBE>
+__global__ __launch_bounds__(kThreads) void merge_pass_kernel(PassParams p) {
+    merge_pass_body<InT, kBE, false>(p);
+}
+// u16 passes (measured: one sub-tile per tile at 128 VGPRs, 4 waves per SIMD, is 45 % slower:
+// the per-tile barriers and look-back dominate)
+template <bool kHashLds>
+__global__ __launch_bounds__(kThreads) void merge_tokens_kernel(PassParams p) {
+    merge_pass_body<uint16_t, true, kHashLds>(p);
 }
 
 // ===========================================================================================
@@ -1513,24 +1549,6 @@ __global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __rest
     }
 }
 
-// Native u16 tokens -> big-endian bytes (the last pass of a multi-pass map found no merge).
-__global__ __launch_bounds__(256) void bswap16_kernel(const uint16_t* __restrict__ in, uint64_t n,
-                                                      uint8_t* __restrict__ out) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t nvec = n / 8;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-        uint4 v = reinterpret_cast<const uint4*>(in)[i];
-        uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = ((w[q] & 0x00FF00FFu) << 8) | ((w[q] >> 8) & 0x00FF00FFu);
-        reinterpret_cast<uint4*>(out)[i] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    for (uint64_t i = nvec * 8 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        out[2 * i] = (uint8_t)(in[i] >> 8);
-        out[2 * i + 1] = (uint8_t)in[i];
-    }
-}
-
 __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
     if (threadIdx.x == 0) flag_error(ctl, sticky, 1u);
 }
@@ -1564,17 +1582,26 @@ static int grid_for(uint32_t ntiles, int device, const void* fn, int threads, in
 
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s) {
     if (p.ntiles == 0) return hipSuccess;
-    const void* fn;
-    if (!input_u16) fn = big_endian ? (const void*)merge_pass_kernel<uint8_t, true> : (const void*)merge_pass_kernel<uint8_t, false>;
-    else fn = big_endian ? (const void*)merge_pass_kernel<uint16_t, true> : (const void*)merge_pass_kernel<uint16_t, false>;
-    const int grid = grid_for(p.ntiles, device, fn, kThreads, (input_u16 ? 2 : 0) + (big_endian ? 1 : 0));
     if (!input_u16) {
+        const void* fn = big_endian ? (const void*)merge_pass_kernel<uint8_t, true> : (const void*)merge_pass_kernel<uint8_t, false>;
+        const int grid = grid_for(p.ntiles, device, fn, kThreads, big_endian ? 1 : 0);
         if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint8_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
         else hipLaunchKernelGGL((merge_pass_kernel<uint8_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
-    } else {
-        if (big_endian) hipLaunchKernelGGL((merge_pass_kernel<uint16_t, true>), dim3(grid), dim3(kThreads), 0, s, p);
-        else hipLaunchKernelGGL((merge_pass_kernel<uint16_t, false>), dim3(grid), dim3(kThreads), 0, s, p);
+        return hipGetLastError();
     }
+    // u16 passes: big-endian in and out; the bucket table in LDS when it fits (then several
+    // workgroups share a CU and cover each other's barriers).  p.ntiles is the upper bound the
+    // input size allows; the kernel reads the actual count from p.n_dev.
+    const bool lds = p.hbytes <= kHashLdsMax;
+    const void* fn = lds ? (const void*)merge_tokens_kernel<true> : (const void*)merge_tokens_kernel<false>;
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 1;
+    const size_t smem = lds ? p.hbytes : 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kThreads, smem) != hipSuccess || occ < 1) occ = 1;
+    long long grid = (long long)cus * occ;
+    if (grid > (long long)p.ntiles) grid = p.ntiles;
+    if (lds) hipLaunchKernelGGL((merge_tokens_kernel<true>), dim3((unsigned)grid), dim3(kThreads), smem, s, p);
+    else hipLaunchKernelGGL((merge_tokens_kernel<false>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
     return hipGetLastError();
 }
 
@@ -1611,13 +1638,5 @@ hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_bswap16(const uint16_t* in, uint64_t n, uint8_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    uint64_t blocks = (n / 8 + 255) / 256;
-    if (blocks < 1) blocks = 1;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(bswap16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
-    return hipGetLastError();
-}
 
 }  // namespace blt
