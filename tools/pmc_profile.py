@@ -69,7 +69,7 @@ def main():
         i = argv.index("--")
         argv, extra = argv[:i], argv[i + 1:]
     a = ap.parse_args(argv)
-    bench_args = extra or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline"]
+    bench_args = extra or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-extra"]
     os.makedirs(a.outdir, exist_ok=True)
     result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}}
     for g in a.groups.split(","):
