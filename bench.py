@@ -277,8 +277,9 @@ def main():
     if os.path.exists(args.traffic):
         with open(args.traffic) as f:
             tj = json.load(f)
-        if tj.get("bytes_per_gpu") == n and tj.get("chunk_size") == CHUNK:
-            traffic = tj.get("hbm_bytes_per_launch")
+        tw = tj.get("workloads", {}).get(args.workload, {})
+        if tw.get("bytes_per_gpu") == n and tw.get("chunk_size") == CHUNK:
+            traffic = tw.get("hbm_bytes_per_launch")
 
     cpu = None
     cpu_opt = None

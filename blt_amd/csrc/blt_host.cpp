@@ -22,6 +22,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/blt_bpe.h"
@@ -238,7 +239,7 @@ struct DevTables {
     uint16_t* dense = nullptr;      // native u16 values, sentinel where absent (general kernel)
     uint16_t* self_ne = nullptr;    // self-token table, native byte order (byte-pass kernel)
     uint16_t* self_be = nullptr;    // self-token table, output (big-endian) byte order
-    uint4* hbuckets = nullptr;      // general map: cuckoo buckets (u16 passes)
+    uint2* hbuckets = nullptr;      // general map: cuckoo buckets (u16 passes)
 };
 
 struct blt_bpe {
@@ -253,8 +254,8 @@ struct blt_bpe {
     // kernel then reads "merge" off the entry's high byte instead of comparing it with a.
     bool hi_merge = true;
     std::vector<uint16_t> self_ne, self_be;
-    // General map (not single_pass): 2-choice cuckoo table of buckets of two slots for the u16
-    // passes (blt::bucket_of), words [key0, val0, key1, val1]; val = BE(value) | 1 << 16.
+    // General map (not single_pass): 2-choice cuckoo table of one-slot buckets for the u16 passes
+    // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31.
     std::vector<uint32_t> hwords;
     uint32_t hmul1 = 0, hmul2 = 0, hshift = 0;
     DevTables dev[kMaxDevices];
@@ -268,47 +269,54 @@ struct blt_bpe {
 
 namespace {
 
-// 2-choice cuckoo placement of the general map (u16 passes): buckets of two slots, load at most
-// one half, multiplicative hashes; new multipliers (and then twice the buckets) until every key
-// has a place.  Empty slots hold a key that is not in the map.
+// 2-choice cuckoo placement of the general map (u16 passes): one-slot buckets [key, value],
+// load at most one half, dot2 hashes of the key's u16 halves (blt::bucket_of); new multipliers
+// (and then twice the buckets) until every key has a place.  The key of (a, b) is the pair's
+// u16 words as stored, BE(a) | BE(b) << 16; empty buckets hold a key that is not in the map.
 bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, blt_bpe* h) {
+    auto be = [](uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); };
+    std::vector<uint32_t> keys, vals;
+    keys.reserve(map.size());
+    vals.reserve(map.size());
+    for (const auto& kv : map) {
+        keys.push_back(be(kv.first >> 16) | (be(kv.first & 0xFFFFu) << 16));
+        vals.push_back(be(kv.second) | 0x80000000u);
+    }
+    std::unordered_set<uint32_t> keyset(keys.begin(), keys.end());
     uint32_t empty = 0xFFFFFFFFu;
-    while (map.count(empty)) --empty;
+    while (keyset.count(empty)) --empty;
     uint32_t log2nb = 2;
-    while ((1u << log2nb) < map.size()) ++log2nb;
+    while ((1ull << log2nb) < 2 * map.size()) ++log2nb;
     uint64_t seed = 0x9E3779B97F4A7C15ull;
     auto next_mul = [&seed]() {
         seed = seed * 6364136223846793005ull + 1442695040888963407ull;
-        return (uint32_t)(seed >> 32) | 1u;
+        return (uint32_t)(seed >> 32) | 0x00010001u;   // two odd 16-bit multipliers
     };
-    for (; log2nb <= 24; ++log2nb) {
+    for (; log2nb <= 25; ++log2nb) {
         const uint32_t nb = 1u << log2nb, shift = 32 - log2nb;
         for (int attempt = 0; attempt < 32; ++attempt) {
             const uint32_t m1 = next_mul(), m2 = next_mul();
-            std::vector<uint32_t> key(2ull * nb, empty), val(2ull * nb, 0);
+            std::vector<uint32_t> key(nb, empty), val(nb, 0);
             bool ok = true;
-            for (const auto& kv : map) {
-                uint32_t k = kv.first, v = ((uint32_t)((kv.second & 0xFF) << 8) | (kv.second >> 8)) | 0x10000u;
+            for (size_t i = 0; i < keys.size() && ok; ++i) {
+                uint32_t k = keys[i], v = vals[i];
                 uint32_t b = blt::bucket_of(k, m1, shift);
                 bool placed = false;
                 for (int kick = 0; kick < 512 && !placed; ++kick) {
-                    const uint32_t b2 = blt::bucket_of(k, m2, shift);
-                    for (uint32_t c : {b, b2})
-                        for (int sl = 0; sl < 2 && !placed; ++sl)
-                            if (key[2 * c + sl] == empty) { key[2 * c + sl] = k; val[2 * c + sl] = v; placed = true; }
-                    if (placed) break;
-                    // evict a slot of b (alternating), carry the evicted key to its other bucket
-                    const uint32_t sl = kick & 1u;
-                    std::swap(k, key[2 * b + sl]);
-                    std::swap(v, val[2 * b + sl]);
-                    const uint32_t o1 = blt::bucket_of(k, m1, shift), o2 = blt::bucket_of(k, m2, shift);
-                    b = (o1 == b) ? o2 : o1;
+                    const uint32_t b1 = blt::bucket_of(k, m1, shift), b2 = blt::bucket_of(k, m2, shift);
+                    if (key[b1] == empty) { key[b1] = k; val[b1] = v; placed = true; break; }
+                    if (key[b2] == empty) { key[b2] = k; val[b2] = v; placed = true; break; }
+                    // evict the occupant of b (alternating between the key's two buckets) and carry
+                    // it to its other bucket
+                    b = (kick & 1) ? b2 : b1;
+                    std::swap(k, key[b]);
+                    std::swap(v, val[b]);
                 }
-                if (!placed) { ok = false; break; }
+                ok = placed;
             }
             if (!ok) continue;
-            h->hwords.assign(4ull * nb, 0);
-            for (uint32_t i = 0; i < 2 * nb; ++i) {
+            h->hwords.assign(2ull * nb, 0);
+            for (uint32_t i = 0; i < nb; ++i) {
                 h->hwords[2 * i] = key[i];
                 h->hwords[2 * i + 1] = val[i];
             }
@@ -449,12 +457,17 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
-    uint64_t ctl, status, total, off_a, off_b, tok_a, tok_b, bytes, zero_bytes;
+    uint64_t ctl, status, total, off_a, off_b, cmap, bytes, zero_bytes;
 };
 
+// Workspace: control block and look-back status words (zeroed before each pass), then for a
+// general map the pass totals and done flag, two chunk-offset arrays (the passes alternate) and
+// the chunk map of the u16 scan kernel (one word per kTokRange tokens).  The u16 passes run in
+// place in the caller's output.
 WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     WsLayout L{};
-    const uint64_t tile = single_pass ? std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes) : blt::kTilePosU16;
+    const uint64_t tile = single_pass ? std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes)
+                                      : std::min<uint64_t>(blt::kTilePosTok, blt::kTilePosBytes);
     L.ntiles = (n + tile - 1) / tile;
     L.nchunks = n ? (n + cs - 1) / cs : 0;
     L.ctl = 0;
@@ -463,10 +476,8 @@ WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     L.total = L.zero_bytes;   // u64 [2] pass totals (alternating), u32 done flag, pad: 32 bytes
     L.off_a = L.total + 32;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
-    L.tok_a = L.off_b + up16(8 * (L.nchunks + 1));
-    L.tok_b = L.tok_a;
-    // a general map's passes alternate between the caller's output and one workspace buffer
-    L.bytes = single_pass ? L.tok_a : L.tok_a + up16(2 * n);
+    L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
+    L.bytes = single_pass ? L.cmap : L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
     return L;
 }
 
@@ -480,7 +491,8 @@ int ctl_error(const uint32_t* ctl) {
     if (ctl[1])
         return fail(BLT_E_IO,
                     "merge-scan device check failed (flags 0x%x: 1 look-back timeout, 2 output range, 4 prefix "
-                    "invariant; first at tile %u sub-tile %u, O=%llu, value=%llu, C=%u)",
+                    "invariant, 8 workgroup wait timeout, 16 chunk map; first at tile %u sub-tile %u, O=%llu, "
+                    "value=%llu, C=%u)",
                     ctl[1], ctl[2] ? ctl[2] - 1 : 0, ctl[3], (unsigned long long)ctl[4] | ((unsigned long long)ctl[5] << 32),
                     (unsigned long long)ctl[6] | ((unsigned long long)ctl[7] << 32), ctl[8]);
     return 0;
@@ -501,11 +513,14 @@ struct Chain {
     uint32_t* done = nullptr;         // set by a pass that merged nothing
 };
 
+// tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
-             uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr) {
+             uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr,
+             bool tok_scan = false) {
     const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->self_ok;   // byte-pass fast kernel
-    const uint64_t tile = columnar ? blt::kTilePosBytes : in_u16 ? blt::kTilePosU16 : blt::kTilePos;
+    const uint64_t tile = columnar ? blt::kTilePosBytes
+                                   : in_u16 ? (tok_scan ? blt::kTilePosTok : blt::kTilePosU16) : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
     if (!ws_zeroed) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
@@ -540,7 +555,9 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     }
     p.debug = g_debug_tiles;
     p.sticky = h->sticky;
+    p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));
+    else if (in_u16 && tok_scan) HIP_TRY(blt::launch_scan_tokens(p, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }
@@ -578,28 +595,30 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         return 0;
     }
 
-    // General map: pass 1 on bytes, then passes on big-endian u16 tokens until one merges
-    // nothing (tokenizer.rs:63-86; a pass that merges nothing leaves the tokens, so running it
-    // for every chunk once the slowest chunk is done changes nothing).  Passes alternate between
-    // d_out and one workspace buffer; the pass that merges nothing writes its input unchanged, so
-    // both then hold the result.  The host enqueues kBatch passes at a time and reads the pass
-    // totals and the done flag once per batch (passes after the done one return at once).
+    // General map: pass 1 on bytes into d_out, then passes on big-endian u16 tokens, in place in
+    // d_out, until one merges nothing (tokenizer.rs:63-86; a pass that merges nothing leaves the
+    // tokens, so running it for every chunk once the slowest chunk is done changes nothing).  The
+    // chunk offsets alternate between two arrays.  The host enqueues kBatch passes at a time and
+    // reads the pass totals and the done flag once per batch (passes after the done one return at
+    // once).  u16 pass k runs on the scan kernel while every chunk holds >= kTokRange tokens
+    // (a pass at most halves a chunk: chunk_size >> k), else on the generic kernel.
     constexpr int kBatch = 4;
-    uint8_t* tok[2] = {d_out, ws + L.tok_a};
+    if (L.nchunks >= (1ull << 32)) return fail(BLT_E_INVALID_INPUT, "too many chunks");
     uint64_t* off[2] = {d_chunk_off ? d_chunk_off : reinterpret_cast<uint64_t*>(ws + L.off_a),
                         reinterpret_cast<uint64_t*>(ws + L.off_b)};
     uint64_t* tot = reinterpret_cast<uint64_t*>(ws + L.total);
     uint32_t* done = reinterpret_cast<uint32_t*>(ws + L.total + 16);
     HIP_TRY(hipMemsetAsync(tot, 0, 32, s));
-    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, tok[0], true, 2 * n, off[0])) return rc;
+    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0])) return rc;
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
     for (;;) {
         for (int b = 0; b < kBatch; ++b, ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done};
-            if (int rc = run_pass(h, t, dev, s, ws, L, tok[cur], true, n, 0, off[cur], tok[cur ^ 1], true, 2 * n,
-                                  off[cur ^ 1], false, &c))
+            const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
+            if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
+                                  false, &c, scan))
                 return rc;
             cur ^= 1;
         }
@@ -609,6 +628,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if ((uint32_t)rec[2]) break;
         if (k > n + kBatch) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
+    // the pass that merged nothing wrote chunk offsets equal to its input's: both arrays hold them
     if (d_chunk_off && off[0] != d_chunk_off)
         HIP_TRY(hipMemcpyAsync(d_chunk_off, off[0], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
     if (out_tokens) *out_tokens = rec[0];

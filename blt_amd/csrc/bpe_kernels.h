@@ -7,7 +7,9 @@ namespace blt {
 
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
-constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the u16 passes
+constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
+constexpr uint64_t kTilePosTok = 16384;        // tokens per look-back tile of the u16 scan kernel
+constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chunk-map word each)
 constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
@@ -30,14 +32,16 @@ struct PassParams {
     const uint16_t* dense;     // dense byte-pair table (65536 entries, swizzled layout).  General
                                // kernel: native values, sentinel where absent.  Byte-pass kernel:
                                // self-token table (absent (a, b) -> a) in the output byte order
-    const uint4* hbuckets;     // general map (u16 passes): 2-choice cuckoo buckets of two slots,
-                               // [key0, val0, key1, val1]; key = a << 16 | b, val = BE(v) | 1 << 16,
-                               // empty slots hold hempty (a key not in the map) and val 0
-    uint32_t hmul1, hmul2;     // bucket of key: (key * hmul) >> hshift, two choices
+    const uint2* hbuckets;     // general map (u16 passes): 2-choice cuckoo table of one-slot
+                               // buckets [key, val]; key = the pair's u16 words as stored (big-endian
+                               // tokens), BE(a) | BE(b) << 16; val = BE(v) | 1 << 31; empty buckets hold
+                               // a key not in the map and val 0
+    uint32_t hmul1, hmul2;     // bucket of key: dot2(key, hmul) >> hshift (u16 halves), two choices
     uint32_t hshift;
     uint32_t hbytes;           // table bytes (u16 passes stage the table in LDS when it fits)
     const uint64_t* n_dev;     // u16 passes: the token count written by the previous pass (on device)
     uint32_t* done;            // u16 passes: set when a pass merged nothing; later passes return at once
+    uint64_t* cmap;            // u16 scan kernel: chunk-map word per wave range of kTokRange tokens
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
     uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles
                                // (below 2^31), else 0
@@ -56,6 +60,10 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
 // kTilePosBytes positions.
 // hi_merge: every byte-pair merge value is >= 256, so an entry's high byte tells a merge.
 hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s);
+// u16 pass of a general map on the scan kernel (seg::scan_tokens_kernel), in place (p.in may equal
+// p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
+// at least kTokRange tokens.
+hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 // Test hook: runs the kernels' error path once (ctl nullable, sticky the handle's error word).
 hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s);
@@ -71,8 +79,11 @@ constexpr uint32_t kSelfRow = 258;
 constexpr uint32_t kSelfEntries = 256 * kSelfRow;
 inline uint32_t self_index(uint32_t a, uint32_t b) { return a * kSelfRow + b; }
 
-// Bucket of a general-map key (must match bucket_get in bpe_kernels.hip).
-inline uint32_t bucket_of(uint32_t key, uint32_t mul, uint32_t shift) { return (uint32_t)(key * mul) >> shift; }
+// Bucket of a general-map key (must match bucket_get in bpe_kernels.hip): the top bits of
+// v_dot2_u32_u16(key, mul) = lo(key) lo(mul) + hi(key) hi(mul) mod 2^32.
+inline uint32_t bucket_of(uint32_t key, uint32_t mul, uint32_t shift) {
+    return (uint32_t)((key & 0xFFFFu) * (mul & 0xFFFFu) + (key >> 16) * (mul >> 16)) >> shift;
+}
 // Largest general-map table staged in LDS (bytes); larger tables are read from global memory (L2).
 constexpr uint32_t kHashLdsMax = 48u << 10;
 

@@ -274,16 +274,18 @@ template <> struct Seg<uint16_t> {
     static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
 };
 
-// General-map lookup of key a << 16 | b: both candidate buckets are read (no probe loop), a
-// matching slot contributes its value word; found = bit 16, the value is stored big-endian.
+// General-map lookup of the pair key BE(a) | BE(b) << 16 (the two u16 words as stored): both
+// candidate buckets are read (no probe loop); returns the matching bucket's value word,
+// BE(v) | 1 << 31, or 0.  The bucket is the top bits of v_dot2_u32_u16(key, hmul).
+typedef unsigned short hu16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t bucket_hash(uint32_t key, uint32_t mul, uint32_t shift) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(hu16x2, key), __builtin_bit_cast(hu16x2, mul), 0u, false) >> shift;
+}
 template <typename TabPtr>
-__device__ __forceinline__ bool bucket_get(const PassParams& p, TabPtr tab, uint32_t key, uint32_t& vbe) {
-    const uint4 x = tab[(key * p.hmul1) >> p.hshift];
-    const uint4 y = tab[(key * p.hmul2) >> p.hshift];
-    const uint32_t r = (x.x == key ? x.y : 0u) | (x.z == key ? x.w : 0u) | (y.x == key ? y.y : 0u) |
-                       (y.z == key ? y.w : 0u);
-    vbe = r & 0xFFFFu;
-    return (r >> 16) != 0u;
+__device__ __forceinline__ uint32_t bucket_get(const PassParams& p, TabPtr tab, uint32_t key) {
+    const uint2 x = tab[bucket_hash(key, p.hmul1, p.hshift)];
+    const uint2 y = tab[bucket_hash(key, p.hmul2, p.hshift)];
+    return (x.x == key ? x.y : 0u) | (y.x == key ? y.y : 0u);
 }
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t t) { return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu); }
@@ -301,7 +303,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     constexpr uint64_t kTileT = (uint64_t)kSubT * kSubPos;
     constexpr int kGroupsT = kSubT * kWaves;
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[kDense ? 65536 : 8];
-    extern __shared__ uint4 s_hash[];
+    extern __shared__ uint2 s_hash[];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kStageBytes];
     __shared__ WaveFn s_wfn[kGroupsT];
     __shared__ uint32_t s_gin[kGroupsT][4];   // carry-in (H=0, H=1), offset (H=0, H=1)
@@ -329,7 +331,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
         for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
     } else if constexpr (kHashLds) {
-        for (uint32_t i = tid; i < p.hbytes / 16u; i += kThreads) s_hash[i] = p.hbuckets[i];
+        for (uint32_t i = tid; i < p.hbytes / 8u; i += kThreads) s_hash[i] = p.hbuckets[i];
     }
 
     for (;;) {
@@ -362,11 +364,14 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
                     v = s_tab[swz_index(a, b)];
                     hit = (p.sentinel > 0xFFFFu) || (v != p.sentinel);
                 } else {
-                    // tokens are big-endian in memory; the key is native (a << 16 | b), the value
-                    // comes back big-endian
-                    const uint32_t key = (bswap16(a) << 16) | bswap16(b);
-                    if constexpr (kHashLds) hit = bucket_get(p, (const uint4*)s_hash, key, v);
-                    else hit = bucket_get(p, p.hbuckets, key, v);
+                    // tokens are big-endian in memory; the key is the two u16 words as stored, the
+                    // value comes back big-endian
+                    const uint32_t key = a | (b << 16);
+                    uint32_t r;
+                    if constexpr (kHashLds) r = bucket_get(p, (const uint2*)s_hash, key);
+                    else r = bucket_get(p, p.hbuckets, key);
+                    hit = (r >> 31) != 0u;
+                    v = r & 0xFFFFu;
                 }
                 m |= (uint32_t)hit << k;
                 if (k & 1) vals[j][k >> 1] |= v << 16; else vals[j][k >> 1] = v;
@@ -687,13 +692,15 @@ __device__ __forceinline__ uint32_t lane_u32(uint32_t v, int i) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, i);
 }
 
-// Phase-1 state of one tile, per lane.
-struct TileState {
-    uint32_t v[kS][8];   // looked-up tokens, two per register
-    uint32_t mv[kS];     // merge mask | valid mask << 16
-    uint32_t lw[kS];     // carry-in for wave carry-in 0 | for wave carry-in 1 << 1
-    uint32_t ex[kS];     // exclusive prefix count, carry-in 0 | carry-in 1 << 16
+// Phase-1 state of one tile of NS sub-tiles, per lane.
+template <int NS>
+struct TileStateT {
+    uint32_t v[NS][8];   // looked-up tokens, two per register
+    uint32_t mv[NS];     // merge mask | valid mask << 16
+    uint32_t lw[NS];     // carry-in for wave carry-in 0 | for wave carry-in 1 << 1
+    uint32_t ex[NS];     // exclusive prefix count, carry-in 0 | carry-in 1 << 16
 };
+using TileState = TileStateT<kS>;
 
 // ---- per-tile scalars ---------------------------------------------------------------------
 struct TInfo {
@@ -730,6 +737,59 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
     t.bge = (uint32_t)(d > 0x10000ull ? 0x10000ull : d);
     t.k0 = q + (r ? 1u : 0u);
     return t;
+}
+
+// Lane functions (both carry-in hypotheses, packed 16-bit) and wave resolves of NS sub-tiles
+// from their final merge masks m; the sub-tiles' dependency chains (ballots, SGPR carry chain,
+// DPP scan) sit in one basic block so they interleave, and lane 63 writes every wave function
+// (group g = j * kWaves + wave) after them.
+template <int NS>
+__device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t wave, int lane, TileStateT<NS>& st,
+                                              uint32_t (*wfn)[4]) {
+    uint64_t wnonid[NS], wcmask[NS];
+    uint32_t wincl[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        const uint32_t vm = st.mv[j] >> 16;
+        const uint32_t mc = (m[j] & ~1u) | (m[j] << 16);
+        const uint32_t sst = mc & ~pk_shl1(mc);
+        const uint32_t rodd = mc & ~pk_add(mc, sst & 0xAAAAAAAAu);
+        const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
+        const uint32_t L = ~(pk_shl1(M) | 1u) & (vm | (vm << 16));
+        const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
+        // Carries across the wave, on SGPR masks: a lane's carry-in is the carry-out of the
+        // nearest non-identity lane below it (an identity lane merges all 16 positions), or
+        // the wave's carry-in c.  Y = lanes fed carry 1 by such a lane: each D = (non-identity,
+        // carry-out 1) lane's carry runs up through the identity lanes above it and stops at
+        // the next non-identity lane, i.e. the carry chain of M + (D << 1); F = lanes at or below
+        // the lowest non-identity lane, fed by c.
+        const uint64_t nonid = wnonid[j];
+        const uint64_t cmask = __ballot(((M >> 31) & 1u) == 0u);   // carry-out 1 (if not identity)
+        const uint64_t D = cmask & nonid, Mi = ~nonid, A = D << 1;
+        const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
+        const uint64_t F = nonid ? ((nonid & (0ull - nonid)) << 1) - 1ull : ~0ull;
+        const uint64_t CI0 = Y, CI1 = Y | F;
+        // per lane: count under its carry-in, for wave carry-in 0 (low half) and 1 (high half)
+        const uint32_t packed = lane_sel(CI0, cnt0, cnt1) | (lane_sel(CI1, cnt0, cnt1) << 16);
+        const uint32_t incl = wave_scan(packed);
+        st.ex[j] = incl - packed;
+        st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
+        wcmask[j] = cmask;
+        wincl[j] = incl;
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) {
+            const uint32_t g = (uint32_t)j * kWaves + wave;
+            const uint64_t nonid = wnonid[j];
+            wfn[g][0] = nonid == 0;
+            wfn[g][1] = nonid ? (uint32_t)((wcmask[j] >> (63 - __clzll(nonid))) & 1ull) : 0u;
+            wfn[g][2] = wincl[j] & 0xFFFFu;
+            wfn[g][3] = wincl[j] >> 16;
+        }
+    }
 }
 
 // ---- phase 1 of a tile: lookups, lane functions, wave functions ------------------------------
@@ -816,60 +876,15 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             st.mv[j] = m[j] | 0xFFFF0000u;
         }
     }
-    // lane functions (both carry-in hypotheses, packed 16-bit) and wave resolves; the sub-tiles'
-    // dependency chains (ballots, SGPR carry chain, DPP scan) sit in one basic block so they
-    // interleave, and lane 63 writes both wave functions after them
-    uint64_t wnonid[kS], wcmask[kS];
-    uint32_t wincl[kS];
-#pragma unroll
-    for (int j = 0; j < kS; ++j) wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
-#pragma unroll
-    for (int j = 0; j < kS; ++j) {
-        const uint32_t vm = st.mv[j] >> 16;
-        const uint32_t mc = (m[j] & ~1u) | (m[j] << 16);
-        const uint32_t sst = mc & ~pk_shl1(mc);
-        const uint32_t rodd = mc & ~pk_add(mc, sst & 0xAAAAAAAAu);
-        const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
-        const uint32_t L = ~(pk_shl1(M) | 1u) & (vm | (vm << 16));
-        const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
-        // Carries across the wave, on SGPR masks: a lane's carry-in is the carry-out of the
-        // nearest non-identity lane below it (an identity lane merges all 16 positions), or
-        // the wave's carry-in c.  Y = lanes fed carry 1 by such a lane: each D = (non-identity,
-        // carry-out 1) lane's carry runs up through the identity lanes above it and stops at
-        // the next non-identity lane, i.e. the carry chain of M + (D << 1); F = lanes at or below
-        // the lowest non-identity lane, fed by c.
-        const uint64_t nonid = wnonid[j];
-        const uint64_t cmask = __ballot(((M >> 31) & 1u) == 0u);   // carry-out 1 (if not identity)
-        const uint64_t D = cmask & nonid, Mi = ~nonid, A = D << 1;
-        const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
-        const uint64_t F = nonid ? ((nonid & (0ull - nonid)) << 1) - 1ull : ~0ull;
-        const uint64_t CI0 = Y, CI1 = Y | F;
-        // per lane: count under its carry-in, for wave carry-in 0 (low half) and 1 (high half)
-        const uint32_t packed = lane_sel(CI0, cnt0, cnt1) | (lane_sel(CI1, cnt0, cnt1) << 16);
-        const uint32_t incl = wave_scan(packed);
-        st.ex[j] = incl - packed;
-        st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
-        wcmask[j] = cmask;
-        wincl[j] = incl;
-    }
-    if (lane == 63) {
-#pragma unroll
-        for (int j = 0; j < kS; ++j) {
-            const uint32_t g = (uint32_t)j * kWaves + wave;
-            const uint64_t nonid = wnonid[j];
-            wfn[g][0] = nonid == 0;
-            wfn[g][1] = nonid ? (uint32_t)((wcmask[j] >> (63 - __clzll(nonid))) & 1ull) : 0u;
-            wfn[g][2] = wincl[j] & 0xFFFFu;
-            wfn[g][3] = wincl[j] >> 16;
-        }
-    }
+    lane_wave_fns<kS>(m, wave, lane, st, wfn);
 }
 
 // ---- tile resolve (one wave): group carries and offsets, tile function, publish -------------
+template <int NG = kGroups>
 __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane, const uint32_t (*wfn)[4],
                                              uint32_t (*gin)[4], uint32_t* tfn) {
     uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
-    if (lane < kGroups) { gi = wfn[lane][0]; gco = wfn[lane][1]; g0 = wfn[lane][2]; g1 = wfn[lane][3]; }
+    if (lane < NG) { gi = wfn[lane][0]; gco = wfn[lane][1]; g0 = wfn[lane][2]; g1 = wfn[lane][3]; }
     const uint64_t nonid = __ballot(!gi);
     const uint64_t cmask = __ballot(gco);
     const uint64_t below = nonid & ((1ull << lane) - 1ull);
@@ -880,7 +895,7 @@ __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, in
     const uint32_t my = (cin0 ? g1 : g0) | ((cin1 ? g1 : g0) << 16);
     const uint32_t inc = wave_scan(my);
     const uint32_t exc = inc - my;
-    if (lane < kGroups) {
+    if (lane < NG) {
         gin[lane][0] = cin0;
         gin[lane][1] = cin1;
         gin[lane][2] = exc & 0xFFFFu;
@@ -1488,6 +1503,374 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
 }
 
+// ===========================================================================================
+// u16 passes of a general map (tokenizer.rs:63-86, every pass after the first) on the byte
+// pass's structure: tickets, one tile in phase 1 while the previous one is looked back and
+// emitted, barrier-free LDS counters.  The input is the previous pass's big-endian u16 tokens.
+//
+// Geometry: lane l of wave w owns tokens [1024 w + 16 l, +16) of a tile (two 16-byte loads), so a
+// tile is 16 wave ranges of 1024 tokens (32 KiB of input) and has one sub-tile per wave.
+//
+// Lookups: a 2-choice cuckoo table of 8-byte buckets [key, value] (the LDS when it fits, else
+// global memory).  The key of the pair (a, b) is the pair's two u16 words as stored, so an even
+// position's key is the lane's input dword itself and an odd one's is one alignbyte; a bucket is
+// the top bits of one v_dot2_u32_u16 of the key with the host's multiplier pair; the value word
+// is BE(v) | 1 << 31, so one byte permute turns two results into the pair's merge mask.
+//
+// Chunk ends: the chunk starts of this pass are the previous pass's chunk offsets.
+// chunk_map_kernel turns them into one word per wave range (at most one chunk start and one
+// chunk end in 1024 tokens: the host runs this kernel only while every chunk holds at least
+// kTokRange tokens, i.e. chunk_size >> pass >= 1024).
+//
+// In place: the pass may write over its own input.  A tile writes only below the end of its
+// own input, and only after its look-back, i.e. after every earlier tile published its
+// aggregate, which each does after its own loads; so every byte a tile overwrites has been read.
+// A wave range whose output is its input (no merge before it in the buffer and none in it)
+// writes nothing, so a pass that merges nothing (the fixpoint check) only reads.
+// ===========================================================================================
+constexpr uint32_t kTileTok = (uint32_t)kWaves * kWavePos;
+static_assert(kTileTok == kTilePosTok && kWavePos == kTokRange, "token tile geometry");
+static_assert(kS * kWaves <= 64 && kWaves <= 64, "groups");
+
+// Chunk-map word of a wave range: bits 0..10 offset of a chunk start, bit 11 set if there is one;
+// bits 12..22 offset of the last token of a chunk (a start minus one), bit 23 set if there is
+// one; bits 32..63 the start's chunk index.
+constexpr uint32_t kCmStart = 1u << 11, kCmEnd = 1u << 23;
+
+__device__ __forceinline__ uint64_t token_count(const PassParams& p) {
+    return p.n_dev ? __hip_atomic_load(const_cast<uint64_t*>(p.n_dev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p.n;
+}
+__device__ __forceinline__ bool pass_done(const PassParams& p) {
+    return p.done && __hip_atomic_load(p.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
+// One thread per wave range: lower bound of the range start in the chunk starts.
+__global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
+    if (pass_done(p)) return;
+    const uint64_t n = token_count(p);
+    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
+    if (lo >= n) return;
+    const uint64_t* cs = p.cstart;
+    const uint64_t nc = p.nchunks;
+    uint64_t a = 0, b = nc;
+    while (a < b) {
+        const uint64_t mid = (a + b) >> 1;
+        if (cs[mid] < lo) a = mid + 1; else b = mid;
+    }
+    uint64_t w = 0;
+    bool bad = false;
+    if (a < nc && cs[a] < hi) {
+        w |= (cs[a] - lo) | kCmStart | (a << 32);
+        bad |= a + 1 < nc && cs[a + 1] < hi;
+    }
+    const uint64_t e = (a < nc && cs[a] == lo) ? a + 1 : a;   // first chunk start > lo
+    if (e < nc && cs[e] <= hi) {
+        w |= ((cs[e] - 1 - lo) << 12) | kCmEnd;
+        bad |= e + 1 < nc && cs[e + 1] <= hi;
+    }
+    if (bad) flag_error(p.ctl, p.sticky, 16u);   // chunks shorter than a wave range: host bug
+    p.cmap[r] = w;
+}
+
+// Tokens of tile Tn into x (the same straight-line loads as load_tile; near the buffer end the
+// lanes' tokens again one by one), and the wave range's chunk-map word (0 past the end).
+__device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32_t Tn, uint32_t wave, int lane,
+                                         uint32_t (&x)[8], uint32_t& nxt, uint32_t (&cw)[2]) {
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+    const uint64_t tile0 = (uint64_t)Tn * kTileTok;
+    const uint64_t left = n > tile0 ? n - tile0 : 0;
+    const __amdgpu_buffer_rsrc_t rd = rsrc_at(in + 2 * tile0, (2 * left) & ~3ull);
+    const uint32_t wrel = wave * kWavePos;
+    const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
+    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, BLT_LDPOL);
+    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, BLT_LDPOL);
+    x[0] = v0[0]; x[1] = v0[1]; x[2] = v0[2]; x[3] = v0[3];
+    x[4] = v1[0]; x[5] = v1[1]; x[6] = v1[2]; x[7] = v1[3];
+    nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, 0);
+    const uint64_t r0 = (uint64_t)Tn * kWaves, nr = (n + kWavePos - 1) / kWavePos;
+    const __amdgpu_buffer_rsrc_t rm = rsrc_at(p.cmap + r0, nr > r0 ? 8 * (nr - r0) : 0);
+    const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * wave), 0, 0);
+    cw[0] = c[0]; cw[1] = c[1];
+    const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+    if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
+        const __amdgpu_buffer_rsrc_t r = rsrc_at(in + 2 * tile0, 2 * left);
+        nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, 0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            x[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, 0) |
+                   ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, 0) << 16);
+    }
+}
+
+// Lookup of one pair key in the token table: LDS byte address tab (kHashLds) or global memory.
+template <bool kHashLds>
+__device__ __forceinline__ uint32_t tok_get(const PassParams& p, uint32_t tab, uint32_t key) {
+    const uint32_t b1 = bucket_hash(key, p.hmul1, p.hshift), b2 = bucket_hash(key, p.hmul2, p.hshift);
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 x, y;
+    if constexpr (kHashLds) {
+        typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+        x = *(const lds_u32x2*)(uintptr_t)(tab + 8u * b1);
+        y = *(const lds_u32x2*)(uintptr_t)(tab + 8u * b2);
+    } else {
+        const u32x2* g = reinterpret_cast<const u32x2*>(p.hbuckets);
+        x = g[b1];
+        y = g[b2];
+    }
+    return (x[0] == key ? x[1] : 0u) | (y[0] == key ? y[1] : 0u);
+}
+
+// Phase 1 of a wave range of tokens: 16 lookups per lane, the output token of each position if
+// it lands (merged value or the token itself, big-endian, two per register), buffer and chunk
+// ends, then the lane and wave functions (lane_wave_fns).  rn: tokens from the tile start to the
+// buffer end; cwl: low word of the range's chunk-map word.
+template <bool kHashLds>
+__device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, const uint32_t (&x)[8], uint32_t nxt,
+                                           uint32_t rn, uint32_t cwl, uint32_t wave, int lane, TileStateT<1>& st,
+                                           uint32_t (*wfn)[4]) {
+    // next lane's first token (wave_shl:1); lane 63 keeps the token after the wave's range
+    const uint32_t nbw = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false);
+    uint32_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int h = k >> 1;
+        const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
+        r[k] = tok_get<kHashLds>(p, tab, key);
+    }
+    uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        const uint32_t R = __builtin_amdgcn_perm(r[2 * h + 1], r[2 * h], 0x05040100u);     // both values
+        const uint32_t hit = __builtin_amdgcn_perm(r[2 * h + 1], r[2 * h], 0x0B0B0909u);   // bit 31 -> half
+        st.v[0][h] = (hit & R) | (~hit & x[h]);
+        m32 |= (hit & 0x00010001u) << (2 * h);
+    }
+    uint32_t m[1] = {(m32 & 0xFFFFu) | (m32 >> 15)};
+    const uint32_t wrel = wave * kWavePos;
+    const uint32_t rem = rn > wrel ? rn - wrel : 0u;
+    const bool has_end = (cwl & kCmEnd) != 0u;
+    if (rem <= kWavePos || has_end) {   // uniform; rare
+        const int32_t rr = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
+        const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
+        uint32_t mm = m[0] & ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u));
+        uint32_t forced = (rr >= 1 && rr <= 16) ? (1u << (rr - 1)) : 0u;   // the buffer's last token
+        if (has_end) {                                                     // a chunk's last token
+            const uint32_t e = ((cwl >> 12) & 0x7FFu) - 16u * (uint32_t)lane;
+            if (e < 16u) { mm &= ~(1u << e); forced |= 1u << e; }
+        }
+        if (__ballot(forced != 0)) {   // a cut merge emits its own token
+#pragma unroll
+            for (int h = 0; h < 8; ++h) {
+                const uint32_t fm = (((forced >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) |
+                                    (((forced >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
+                st.v[0][h] = (st.v[0][h] & ~fm) | (x[h] & fm);
+            }
+        }
+        m[0] = mm;
+        st.mv[0] = mm | (vmask << 16);
+    } else {
+        st.mv[0] = m[0] | 0xFFFF0000u;
+    }
+    lane_wave_fns<1>(m, wave, lane, st, wfn);
+}
+
+// Emission of a tile's wave range (as emit_tile), its chunk start from the chunk-map word.
+__device__ __forceinline__ void emit_tok(const PassParams& p, uint32_t Tp, uint32_t rn, uint32_t cwl, uint32_t cwh,
+                                         uint32_t wave, int lane, const TileStateT<1>& st, const uint32_t (*gin)[4],
+                                         uint32_t C, uint64_t O, uint8_t* stg) {
+    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+    const uint64_t obase = (2ull * O) & ~15ull;
+    const uint32_t orel = (uint32_t)(2ull * O - obase);
+    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
+    const uint32_t wrel = wave * kWavePos;
+    const uint32_t cg = uni(gin[wave][C]);
+    const uint32_t goff = uni(gin[wave][2 + C]);   // tokens before this wave range in the tile
+    const uint32_t gb = orel + 2u * goff;          // output byte of the wave range, from obase
+    const bool cstart = p.chunk_off && (cwl & kCmStart) != 0u;
+    if (__ballot(st.mv[0] != 0xFFFFFFFFu) == 0) {
+        // dense: every pair merges, so the only possible chunk start is the range's first token
+        if (cstart && lane == 0) p.chunk_off[cwh] = O + goff;
+        emit_dense(st.v[0], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
+        return;
+    }
+    const uint32_t m = st.mv[0] & 0xFFFFu, vmask = st.mv[0] >> 16;
+    const uint32_t c = __builtin_amdgcn_ubfe(st.lw[0], cg, 1);
+    const uint32_t lane_off = cg ? (st.ex[0] >> 16) : (st.ex[0] & 0xFFFFu);
+    const uint32_t mc = c ? m : (m & ~1u);
+    const uint32_t sst = mc & ~(mc << 1);
+    const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
+    const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+    const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
+    if (cstart) {
+        const uint32_t e = (cwl & 0x7FFu) - 16u * (uint32_t)lane;
+        if (e < 16u) p.chunk_off[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+    }
+    const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
+    // in place: output = input when nothing merged before this range or in it
+    const uint32_t rem = rn > wrel ? (rn - wrel < kWavePos ? rn - wrel : kWavePos) : 0u;
+    if (wcnt == rem && O + goff == (uint64_t)Tp * kTileTok + wrel) return;
+    const uint32_t two = (gb & 15u) + 2u * wcnt <= (uint32_t)kStageWave ? 0u : 1u;
+    const uint32_t off32 = two ? uni(lane_u32(lane_off, 32)) : 0u;   // tokens before lane 32
+    const uint32_t stg_lds = lds_addr(stg);
+    for (uint32_t part = 0; part <= two; ++part) {
+        const uint32_t base = part ? off32 : 0u;
+        const uint32_t cnt = two ? (part ? wcnt - off32 : off32) : wcnt;
+        const uint32_t gbp = gb + 2u * base;
+        if (!two || ((uint32_t)lane >> 5) == part) stage_b16(st.v[0], L, stg_lds + (gbp & 15u) + 2u * (lane_off - base));
+        const CopyPart cp = {gbp & ~15u, gbp & 15u, (gbp & 15u) + 2u * cnt};
+        CopyData d;
+        copy_read(stg, cp, lane, d);
+        copy_store(ro, cp, lane, d);
+    }
+}
+
+template <bool kHashLds>
+__global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kWaves][4];
+    __shared__ uint32_t s_gin[kRing][kWaves][4];
+    __shared__ uint32_t s_tfn[kRing][4];
+    __shared__ uint64_t s_O[kRing];
+    __shared__ uint32_t s_C[kRing];
+    __shared__ uint32_t s_tk[kRing];
+    __shared__ uint32_t s_p1cnt[kRing];
+    __shared__ uint32_t s_rdone, s_lbdone, s_tkdone;
+
+    if (pass_done(p)) return;   // an earlier pass merged nothing (uniform over the grid)
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wave = uni((uint32_t)tid >> 6);
+    const uint64_t n = uni64(token_count(p));
+    const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
+    auto rn_of = [&](uint32_t T) {
+        const uint64_t l = n - (uint64_t)T * kTileTok;
+        return (uint32_t)(l > 0x7FFFFFFFull ? 0x7FFFFFFFull : l);
+    };
+
+    if (tid == 0) {
+        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);
+        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);
+        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
+        s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
+    }
+    if constexpr (kHashLds) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
+        uint4* dst = reinterpret_cast<uint4*>(s_tokhash);
+        for (uint32_t i = tid; i < p.hbytes / 16u; i += kThreads) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint32_t tab = kHashLds ? uni(lds_addr(s_tokhash)) : 0u;
+    uint32_t T = uni(s_tk[kRing - 2]);
+    uint32_t Tp = kNone;
+    uint32_t Tq = uni(s_tk[kRing - 1]);
+    if (T >= ntiles || Tq >= ntiles) Tq = kNone;
+    __syncthreads();
+
+    uint32_t xa[8], xb[8], na = 0, nb = 0, ca[2] = {0u, 0u}, cb[2] = {0u, 0u};
+    if (T < ntiles) load_tok(p, n, T, wave, lane, xa, na, ca);
+    TileStateT<1> sa, sb;
+    uint64_t lbs[kLbWin];
+    uint32_t it = 0;
+    uint32_t cwpl = 0, cwph = 0;   // Tp's chunk-map word
+
+    auto step = [&](uint32_t (&x)[8], uint32_t& nxt, uint32_t (&cw)[2], uint32_t (&xq)[8], uint32_t& nxtq,
+                    uint32_t (&cwq)[2], TileStateT<1>& sc, const TileStateT<1>& sp) {
+        const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map word have landed
+        const uint32_t cwl = uni(cw[0]), cwh = uni(cw[1]);
+        if (Tq < ntiles) load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
+        uint32_t tk = kNone;
+        if (tid == 64 && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
+        asm volatile("" ::: "memory");
+
+        bool lbw = wave == 0;
+        if (T < ntiles) {
+            if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+            phase1_tok<kHashLds>(p, tab, x, nxt, rn_of(T), cwl, wave, lane, sc, s_wfn[slot]);
+            __builtin_amdgcn_s_setprio(0);
+            uint32_t old = 0;
+            if (lane == 0)
+                old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = uni(old);
+            lbw = old == (uint32_t)kWaves * (it / kRing);
+            if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
+                resolve_tile<kWaves>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                if (lane == 0) lds_release(&s_rdone, it + 1u);
+            }
+        }
+
+        if (lbw && Tp < ntiles) {
+            uint32_t C = 1u, how = 0xFFFFu, spins = 0;
+            uint64_t O = 0ull;
+            const bool lb = Tp > 0;
+            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            wait_ge(p, &s_rdone, it);
+            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+            if (lane == 0) {
+                const uint64_t end = O + (C == 1u ? tf3 : tf2);
+                if (C > 1u || O > (uint64_t)Tp * kTileTok || end > n) {
+                    if (C <= 1u) record_error(p, 4u, Tp, 0xFFu, O, end, C);
+                    O = 0; C = 2u;
+                }
+                s_C[pslot] = C;
+                s_O[pslot] = O;
+                lds_release(&s_lbdone, it + 1u);
+                const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin));
+                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
+                if (Tp == ntiles - 1) {
+                    *p.total = fin;
+                    if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
+                    if (p.done && fin == n) *p.done = 1u;   // merged nothing: the fixpoint
+                }
+                if (p.debug) {
+                    uint64_t* d = p.debug + 4ull * Tp;
+                    d[0] = O;
+                    d[1] = ((uint64_t)C << 32) | how;
+                    d[2] = ((uint64_t)tf3 << 32) | tf2;
+                    d[3] = ((uint64_t)tf1 << 32) | tf0;
+                }
+            }
+        }
+
+        if (Tp < ntiles) {
+            wait_ge(p, &s_lbdone, it + 1u);
+            if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
+            const uint32_t Cp = uni(s_C[pslot]);
+            if (Cp <= 1u)
+                emit_tok(p, Tp, rn_of(Tp), cwpl, cwph, wave, lane, sp, s_gin[pslot], Cp, uni64(s_O[pslot]),
+                         s_stage[wave]);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        if (tid == 64) {
+            s_tk[slot] = tk;
+            lds_release(&s_tkdone, it + 1u);
+        }
+        uint32_t Tr = kNone;
+        if (Tq < ntiles) {
+            wait_ge(p, &s_tkdone, it + 1u);
+            Tr = uni(s_tk[slot]);
+            if (Tr >= ntiles) Tr = kNone;
+        }
+        cwpl = cwl;
+        cwph = cwh;
+        Tp = T;
+        T = Tq;
+        Tq = Tr;
+        ++it;
+    };
+    for (;;) {
+        if (!(T < ntiles || Tp < ntiles)) break;
+        step(xa, na, ca, xb, nb, cb, sa, sb);
+        if (!(T < ntiles || Tp < ntiles)) break;
+        step(xb, nb, cb, xa, na, ca, sb, sa);
+    }
+}
+
 }  // namespace seg
 
 // Byte -> big-endian u16 (BasicTokenizationStrategy, tokenizer.rs:108-124).  A streaming copy
@@ -1621,6 +2004,21 @@ hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, 
         if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<false, true>), g, b, 0, s, p);
         else hipLaunchKernelGGL((seg::scan_bytes_kernel<false, false>), g, b, 0, s, p);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
+    if (p.n == 0) return hipSuccess;
+    // p.n bounds the token count the kernels read from p.n_dev
+    const uint64_t ranges = (p.n + kTokRange - 1) / kTokRange;
+    hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
+    const bool lds = p.hbytes <= kHashLdsMax;
+    const void* fn = lds ? (const void*)seg::scan_tokens_kernel<true> : (const void*)seg::scan_tokens_kernel<false>;
+    const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
+    const int grid = grid_for(ntiles, device, fn, seg::kThreads, lds ? 2 : 3);
+    const size_t smem = lds ? p.hbytes : 0;
+    if (lds) hipLaunchKernelGGL((seg::scan_tokens_kernel<true>), dim3((unsigned)grid), dim3(seg::kThreads), smem, s, p);
+    else hipLaunchKernelGGL((seg::scan_tokens_kernel<false>), dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
     return hipGetLastError();
 }
 

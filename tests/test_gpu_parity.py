@@ -446,3 +446,103 @@ def test_concurrent_full_size_chunks():
         th.join(timeout=100)
     assert not any(th.is_alive() for th in threads)
     assert not errors, errors
+
+
+# ---- u16 passes of general maps on the token scan kernel (seg::scan_tokens_kernel) ----------
+TOK_TILE = 16384  # tokens per tile of the token scan kernel (bpe_kernels.h kTilePosTok)
+CHAINED_TEXT_MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259,
+                    (259, 104): 260}
+
+
+@pytest.mark.parametrize("cs", [4096, 4097, 8192, 65536 + 3, 1 << 20, 3 << 20])
+def test_token_scan_chunk_geometry(cs):
+    """Chunk ends of the u16 passes: pass k runs on the scan kernel while cs >> k >= 1024 tokens
+    (cs = 4096: passes 1-2, then the generic kernel), with one chunk-map word per 1024 tokens."""
+    text = synth.text((3 << 20) + 11, seed=21)
+    s = blt_amd.BpeStrategy(CHAINED_TEXT_MAP)
+    got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(CHAINED_TEXT_MAP).run(text, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("n", [1023, 1024, 1025, 2 * 1024 + 17, TOK_TILE - 1, TOK_TILE, TOK_TILE + 1,
+                               2 * TOK_TILE + 16, 5 * TOK_TILE + 1000, 40 * TOK_TILE + 3])
+def test_token_scan_buffer_ends(n):
+    """Token counts around wave-range (1024) and tile (16384) edges: "aa" -> 256 on pass 1 and
+    (256, 256) -> 257, (257, 257) -> 258 on the u16 passes, with a lone byte at every tenth slot."""
+    rng = np.random.default_rng(n)
+    data = np.full(2 * n + 1, 97, np.uint8)
+    data[rng.integers(0, data.size, data.size // 10)] = 98
+    m = {(97, 97): 256, (256, 256): 257, (257, 257): 258, (98, 258): 259}
+    s = blt_amd.BpeStrategy(m)
+    got = s.process_chunks(data, 1 << 22)
+    exp = O.COracle(m).run(data, 1 << 22, threads=4)
+    assert np.array_equal(got, exp)
+
+
+def test_token_scan_global_table():
+    """A general map too large for the LDS table (> 48 KiB of buckets): lookups from global
+    memory."""
+    letters = range(97, 123)
+    m = {}
+    for i, (a, b) in enumerate((a, b) for a in letters for b in letters):
+        m[(a, b)] = 256 + i
+    for i in range(676):
+        for c in (97, 101, 105, 111, 117):
+            m[(256 + i, c)] = 1000 + 5 * i + (c % 5)
+    assert len(m) > 3072
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    rng = np.random.default_rng(3)
+    data = rng.integers(97, 123, (2 << 20) + 5, dtype=np.uint8)
+    got, lens = s.process_chunks(data, 1 << 19, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, 1 << 19, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("where", [0.0, 0.5, 0.97, 1.0])
+def test_token_scan_in_place_prefix(where):
+    """The u16 passes run in place and skip the wave ranges whose output is their input: the
+    second pass's only merges sit after a prefix of `where` of the buffer (1.0: none, the
+    fixpoint pass is read-only)."""
+    n = 6 << 20
+    data = np.frombuffer(b"xy" * (n // 2), np.uint8).copy()   # pass 1: "xy" -> 256 everywhere
+    k = int(where * n) & ~1
+    if k < n:
+        data[k:k + 4] = np.frombuffer(b"abab", np.uint8)      # pass 1: "ab" -> 257; pass 2: 257 257 -> 258
+    m = {(120, 121): 256, (97, 98): 257, (257, 257): 258}
+    s = blt_amd.BpeStrategy(m)
+    for cs in (1 << 20, n):
+        got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp)
+        assert np.array_equal(lens, elens)
+
+
+def test_token_scan_device_api_in_place():
+    """encode_device on a general map: the u16 passes work in the caller's output buffer; the
+    chunk offsets and the token count match the oracle, and repeated async calls agree."""
+    import torch
+    data = synth.text((5 << 20) + 3, seed=8)
+    s = blt_amd.BpeStrategy(CHAINED_TEXT_MAP)
+    cs = 1 << 20
+    n = data.size
+    nchunks = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    d_off = torch.zeros(nchunks + 1, dtype=torch.int64, device="cuda")
+    ws_b = s.workspace_size(n, cs)
+    assert ws_b < n  # no token buffer in the workspace: the passes run in place
+    ws = torch.empty(ws_b, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    exp, elens = O.COracle(CHAINED_TEXT_MAP).run(data, cs, threads=8, return_lens=True)
+    for _ in range(3):
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), ws_b, stream,
+                              d_off.data_ptr(), sync=True)
+        assert 2 * tok == exp.size
+        assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp)
+        offs = d_off.cpu().numpy()
+        assert offs[-1] == tok
+        assert np.array_equal(np.diff(offs) * 2, elens)
