@@ -255,7 +255,8 @@ struct blt_bpe {
     bool hi_merge = true;
     std::vector<uint16_t> self_ne, self_be;
     // General map (not single_pass): 2-choice cuckoo table of one-slot buckets for the u16 passes
-    // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31.
+    // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31
+    // | 1 << 30 when the value is a component of some key.
     std::vector<uint32_t> hwords;
     uint32_t hmul1 = 0, hmul2 = 0, hshift = 0;
     DevTables dev[kMaxDevices];
@@ -273,14 +274,16 @@ namespace {
 // load at most one half, dot2 hashes of the key's u16 halves (blt::bucket_of); new multipliers
 // (and then twice the buckets) until every key has a place.  The key of (a, b) is the pair's
 // u16 words as stored, BE(a) | BE(b) << 16; empty buckets hold a key that is not in the map.
-bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, blt_bpe* h) {
+// Values carry bit 30 when the merged token is a component of some key (is_comp): the u16 scan
+// kernel stops the passes after one that made no such token.
+bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, const std::vector<uint8_t>& is_comp, blt_bpe* h) {
     auto be = [](uint32_t v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); };
     std::vector<uint32_t> keys, vals;
     keys.reserve(map.size());
     vals.reserve(map.size());
     for (const auto& kv : map) {
         keys.push_back(be(kv.first >> 16) | (be(kv.first & 0xFFFFu) << 16));
-        vals.push_back(be(kv.second) | 0x80000000u);
+        vals.push_back(be(kv.second) | 0x80000000u | (is_comp[kv.second] ? 0x40000000u : 0u));
     }
     std::unordered_set<uint32_t> keyset(keys.begin(), keys.end());
     uint32_t empty = 0xFFFFFFFFu;
@@ -381,7 +384,7 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
     }
     h->self_be.resize(blt::kSelfEntries);
     for (uint32_t i = 0; i < blt::kSelfEntries; ++i) h->self_be[i] = bswap(h->self_ne[i]);
-    if (!h->single_pass && !build_buckets(map, h.get())) return fail(BLT_E_NOMEM, "cannot place the merge map in a hash table");
+    if (!h->single_pass && !build_buckets(map, is_comp, h.get())) return fail(BLT_E_NOMEM, "cannot place the merge map in a hash table");
     *out = h.release();
     return 0;
 }
@@ -451,6 +454,9 @@ int sticky_check(const blt_bpe* h) {
 
 // Test hook: per-tile look-back records (blt_debug_set_tile_record).
 uint64_t* g_debug_tiles = nullptr;
+// Test hook: u16 passes the calling thread's last synchronous general-map encode ran before the
+// chain stopped (blt_debug_last_u16_passes).
+thread_local uint32_t t_last_u16_passes = 0;
 
 // ---- workspace layout -------------------------------------------------------------------
 inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -510,7 +516,8 @@ int check_ctl(uint8_t* ws, hipStream_t s) {
 struct Chain {
     const uint64_t* n_in = nullptr;   // count written by the previous pass
     uint64_t* n_out = nullptr;        // this pass's count
-    uint32_t* done = nullptr;         // set by a pass that merged nothing
+    uint32_t* done = nullptr;         // set to its pass_id by the last pass that can merge anything
+    uint32_t pass_id = 0;             // 1, 2, ...
 };
 
 // tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).
@@ -523,7 +530,8 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
                                    : in_u16 ? (tok_scan ? blt::kTilePosTok : blt::kTilePosU16) : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
-    if (!ws_zeroed) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
+    // (the u16 scan's chunk-map kernel zeroes the control block and status words itself)
+    if (!ws_zeroed && !(in_u16 && tok_scan)) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
     blt::PassParams p{};
     p.in = in;
     p.n = n;
@@ -539,6 +547,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     if (chain) {
         p.n_dev = chain->n_in;
         p.done = chain->done;
+        p.pass_id = chain->pass_id;
     }
     p.ntiles = (uint32_t)ntiles;
     p.sentinel = h->sentinel;
@@ -598,11 +607,13 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // General map: pass 1 on bytes into d_out, then passes on big-endian u16 tokens, in place in
     // d_out, until one merges nothing (tokenizer.rs:63-86; a pass that merges nothing leaves the
     // tokens, so running it for every chunk once the slowest chunk is done changes nothing).  The
-    // chunk offsets alternate between two arrays.  The host enqueues kBatch passes at a time and
+    // chunk offsets alternate between two arrays.  The host enqueues a batch of passes at a time and
     // reads the pass totals and the done flag once per batch (passes after the done one return at
     // once).  u16 pass k runs on the scan kernel while every chunk holds >= kTokRange tokens
-    // (a pass at most halves a chunk: chunk_size >> k), else on the generic kernel.
-    constexpr int kBatch = 4;
+    // (a pass at most halves a chunk: chunk_size >> k), else on the generic kernel.  The scan
+    // kernel also ends the chain after a pass none of whose merges made a key component, so
+    // most maps finish after one u16 pass: the first batch is 2 passes, later ones 4.  The done
+    // word holds the pass k after which nothing merges; its totals and chunk offsets are [k & 1].
     if (L.nchunks >= (1ull << 32)) return fail(BLT_E_INVALID_INPUT, "too many chunks");
     uint64_t* off[2] = {d_chunk_off ? d_chunk_off : reinterpret_cast<uint64_t*>(ws + L.off_a),
                         reinterpret_cast<uint64_t*>(ws + L.off_b)};
@@ -613,9 +624,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
-    for (;;) {
-        for (int b = 0; b < kBatch; ++b, ++k) {
-            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done};
+    for (int batch = 2;; batch = 4) {
+        for (int b = 0; b < batch; ++b, ++k) {
+            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
                                   false, &c, scan))
@@ -626,12 +637,13 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = sticky_check(h)) return rc;
         if ((uint32_t)rec[2]) break;
-        if (k > n + kBatch) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
+        if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
-    // the pass that merged nothing wrote chunk offsets equal to its input's: both arrays hold them
-    if (d_chunk_off && off[0] != d_chunk_off)
-        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[0], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
-    if (out_tokens) *out_tokens = rec[0];
+    t_last_u16_passes = (uint32_t)rec[2];
+    const uint32_t last = (uint32_t)rec[2] & 1u;   // the arrays the final pass wrote
+    if (d_chunk_off && off[last] != d_chunk_off)
+        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[last], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+    if (out_tokens) *out_tokens = rec[last];
     return 0;
 }
 
@@ -1125,6 +1137,10 @@ int blt_bpe_check_workspace(void* d_ws, void* stream) {
 // Not in the public header: a test hook that makes every merge pass record, per tile, its
 // carry-in/offset/look-back lane and both hypothesis counts into a device buffer.
 void blt_debug_set_tile_record(uint64_t* d_buf) { g_debug_tiles = d_buf; }
+
+// Not in the public header: the number of u16 passes the calling thread's last general-map
+// encode ran (the pass after which nothing can merge; later enqueued passes returned at once).
+uint32_t blt_debug_last_u16_passes(void) { return t_last_u16_passes; }
 
 // Not in the public header: a test hook that runs the kernels' device-error path (the one a
 // look-back timeout takes) for handle h on the current device and stream, setting error bit 1 in

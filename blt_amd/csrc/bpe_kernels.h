@@ -34,13 +34,17 @@ struct PassParams {
                                // self-token table (absent (a, b) -> a) in the output byte order
     const uint2* hbuckets;     // general map (u16 passes): 2-choice cuckoo table of one-slot
                                // buckets [key, val]; key = the pair's u16 words as stored (big-endian
-                               // tokens), BE(a) | BE(b) << 16; val = BE(v) | 1 << 31; empty buckets hold
-                               // a key not in the map and val 0
+                               // tokens), BE(a) | BE(b) << 16; val = BE(v) | 1 << 31 | live << 30 (live:
+                               // v is a component of some key); empty buckets hold a key not in the
+                               // map and val 0
     uint32_t hmul1, hmul2;     // bucket of key: dot2(key, hmul) >> hshift (u16 halves), two choices
     uint32_t hshift;
     uint32_t hbytes;           // table bytes (u16 passes stage the table in LDS when it fits)
     const uint64_t* n_dev;     // u16 passes: the token count written by the previous pass (on device)
-    uint32_t* done;            // u16 passes: set when a pass merged nothing; later passes return at once
+    uint32_t* done;            // u16 passes: set to pass_id by the pass after which the next merges
+                               // nothing (it merged nothing, or none of its merges made a key
+                               // component); later passes return at once
+    uint32_t pass_id;          // u16 passes: 1, 2, ... (pass k writes totals and chunk offsets [k & 1])
     uint64_t* cmap;            // u16 scan kernel: chunk-map word per wave range of kTokRange tokens
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
     uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles

@@ -102,9 +102,12 @@ __device__ __forceinline__ void resolve_wave(uint32_t ident, uint32_t cout, uint
 
 // ---- status words of the decoupled look-back (one per tile) -------------------------------
 // bits 63..62: 0 empty, 1 aggregate, 2 inclusive prefix.
-//  aggregate: bit 61 carry-out for carry-in 1, bit 60 for carry-in 0, bits 30..59 count for
-//             carry-in 1, bits 0..29 count for carry-in 0.
-//  inclusive: bit 61 carry into the next tile, bits 0..60 tokens before the next tile.
+//  aggregate: bit 61 carry-out for carry-in 1, bit 60 for carry-in 0, bit 59 live (u16 scan
+//             kernel: the tile has a merge whose value is a key component), bits 30..58 count
+//             for carry-in 1, bits 0..29 count for carry-in 0.
+//  inclusive: bit 61 carry into the next tile, bit 60 live (some tile up to this one is live),
+//             bits 0..59 tokens before the next tile.
+constexpr uint64_t kStLiveAgg = 1ull << 59, kStLiveIncl = 1ull << 60;
 __device__ __forceinline__ uint64_t st_agg(uint32_t co0, uint32_t co1, uint32_t c0, uint32_t c1) {
     return (1ull << 62) | ((uint64_t)co1 << 61) | ((uint64_t)co0 << 60) | ((uint64_t)c1 << 30) | c0;
 }
@@ -448,7 +451,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
                 if (T == p.ntiles - 1) {
                     *p.total = end;
                     if (p.chunk_off) p.chunk_off[p.nchunks] = end;
-                    if (!kDense && p.done && end == p.n) *p.done = 1u;   // no merge: the fixpoint
+                    if (!kDense && p.done && end == p.n) *p.done = p.pass_id;   // no merge: the fixpoint
                 }
             }
         }
@@ -745,7 +748,7 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
 // (group g = j * kWaves + wave) after them.
 template <int NS>
 __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t wave, int lane, TileStateT<NS>& st,
-                                              uint32_t (*wfn)[4]) {
+                                              uint32_t (*wfn)[4], uint32_t wlive = 0u) {
     uint64_t wnonid[NS], wcmask[NS];
     uint32_t wincl[NS];
 #pragma unroll
@@ -784,7 +787,7 @@ __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t 
         for (int j = 0; j < NS; ++j) {
             const uint32_t g = (uint32_t)j * kWaves + wave;
             const uint64_t nonid = wnonid[j];
-            wfn[g][0] = nonid == 0;
+            wfn[g][0] = (nonid == 0) | (wlive << 1);   // identity | live << 1
             wfn[g][1] = nonid ? (uint32_t)((wcmask[j] >> (63 - __clzll(nonid))) & 1ull) : 0u;
             wfn[g][2] = wincl[j] & 0xFFFFu;
             wfn[g][3] = wincl[j] >> 16;
@@ -880,11 +883,15 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 }
 
 // ---- tile resolve (one wave): group carries and offsets, tile function, publish -------------
-template <int NG = kGroups>
+// kLive (u16 scan kernel): the groups' live bits (wfn[g][0] bit 1) are ORed into the tile's
+// status word and into tfn[0] bit 1.
+template <int NG = kGroups, bool kLive = false>
 __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane, const uint32_t (*wfn)[4],
                                              uint32_t (*gin)[4], uint32_t* tfn) {
     uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
     if (lane < NG) { gi = wfn[lane][0]; gco = wfn[lane][1]; g0 = wfn[lane][2]; g1 = wfn[lane][3]; }
+    const uint32_t tlive = kLive ? (__ballot((gi >> 1) & 1u) != 0) : 0u;
+    if (kLive) gi &= 1u;
     const uint64_t nonid = __ballot(!gi);
     const uint64_t cmask = __ballot(gco);
     const uint64_t below = nonid & ((1ull << lane) - 1ull);
@@ -907,9 +914,10 @@ __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, in
     const uint32_t tcout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
     const uint32_t co0 = tident ? 0u : tcout, co1 = tident ? 1u : tcout;
     if (lane == 0) {
-        tfn[0] = co0; tfn[1] = co1; tfn[2] = tot0; tfn[3] = tot1;
+        tfn[0] = co0 | (tlive << 1); tfn[1] = co1; tfn[2] = tot0; tfn[3] = tot1;
         // tile 0 starts with carry 1 at offset 0: its inclusive prefix is known at once
-        st_publish(p.status + T, T == 0 ? st_incl(co1, tot1) : st_agg(co0, co1, tot0, tot1));
+        st_publish(p.status + T, T == 0 ? st_incl(co1, tot1) | (tlive ? kStLiveIncl : 0ull)
+                                        : st_agg(co0, co1, tot0, tot1) | (tlive ? kStLiveAgg : 0ull));
     }
 }
 
@@ -926,8 +934,10 @@ __device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lan
 
 // Function of the aggregates in lanes [0, lim) of one window (lane 0 newest) applied to
 // carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.
-__device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot) {
+__device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot,
+                                              uint32_t& live) {
     const bool in = lane < lim;
+    live |= __ballot(in && (s & kStLiveAgg) != 0) != 0;
     const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
     const uint32_t co0 = (hi >> 28) & 1u;
     const bool ident = ((hi >> 28) & 3u) == 2u;   // co0 = 0, co1 = 1
@@ -946,7 +956,7 @@ __device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uin
         const uint64_t older = nonid & ~((~0ull) >> (63 - lane));
         cin = older ? (uint32_t)((comask >> __builtin_ctzll(older)) & 1ull) : c;
     }
-    const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x3FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
+    const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x1FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
     tot += lane_u32(wave_scan(cnt), 63);
     return nonid ? (uint32_t)((comask >> __builtin_ctzll(nonid)) & 1ull) : c;
 }
@@ -956,8 +966,9 @@ struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never 
     uint64_t t0, t1;
 };
 
+// live: OR of the live bits of every tile before Tp (u16 scan kernel; 0 in the byte pass).
 __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (&s)[kLbWin], uint32_t& C,
-                          uint64_t& O, uint32_t& how, uint32_t& spins, uint32_t* bad_out = nullptr) {
+                          uint64_t& O, uint32_t& how, uint32_t& spins, uint32_t& live, uint32_t* bad_out = nullptr) {
     TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
     int64_t k = (int64_t)Tp - 1;
     uint32_t rounds = 0;
@@ -1005,7 +1016,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 uint32_t c = (uint32_t)h;
                 uint64_t t = 0;
 #pragma unroll
-                for (int q = kLbWin - 1; q >= 0; --q) c = win_apply(s[q], 64, lane, c, t);
+                for (int q = kLbWin - 1; q >= 0; --q) c = win_apply(s[q], 64, lane, c, t, live);
                 t += c ? acc.t1 : acc.t0;
                 if (h == 0) { w.co0 = c ? acc.co1 : acc.co0; w.t0 = t; }
                 else { w.co1 = c ? acc.co1 : acc.co0; w.t1 = t; }
@@ -1024,10 +1035,11 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
             if (q == qs) {
                 const uint64_t sf = ((uint64_t)lane_u32((uint32_t)(s[q] >> 32), f) << 32) | lane_u32((uint32_t)s[q], f);
                 c = (uint32_t)(sf >> 61) & 1u;
-                off = sf & ((1ull << 61) - 1ull);
-                c = win_apply(s[q], f, lane, c, off);
+                off = sf & (kStLiveIncl - 1ull);
+                live |= (sf & kStLiveIncl) != 0;
+                c = win_apply(s[q], f, lane, c, off, live);
             } else {
-                c = win_apply(s[q], 64, lane, c, off);
+                c = win_apply(s[q], 64, lane, c, off, live);
             }
         }
         O = off + (c ? acc.t1 : acc.t0);
@@ -1410,7 +1422,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // ---- carry-in and offset of Tp, by the first wave to finish phase 1: its snapshot is
         // the freshest that still lands before the slower waves finish (~0.5 us round trip)
         if (lbw && Tp < ntiles) {
-            uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0;
+            uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0, live = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
@@ -1419,7 +1431,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             wait_ge(p, &s_rdone, it);
             const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
             const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, kTiming ? &bad : nullptr);
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live, kTiming ? &bad : nullptr);
             if (lane == 0) {
                 const uint64_t end = O + (C == 1u ? tf3 : tf2);
                 // a failed tile (flagged) writes nothing (C = 2) and publishes a prefix only so its
@@ -1544,11 +1556,15 @@ __device__ __forceinline__ bool pass_done(const PassParams& p) {
     return p.done && __hip_atomic_load(p.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
 }
 
-// One thread per wave range: lower bound of the range start in the chunk starts.
+// One thread per wave range: lower bound of the range start in the chunk starts.  It also zeroes
+// the scan's control block and status words (one per kTileTok tokens, so the wave ranges cover
+// them): the previous pass has finished with them.
 __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     if (pass_done(p)) return;
     const uint64_t n = token_count(p);
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
+    if (r < kCtlBytes / 4) p.ctl[r] = 0u;
     const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
     if (lo >= n) return;
     const uint64_t* cs = p.cstart;
@@ -1638,6 +1654,12 @@ __device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, co
         const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
         r[k] = tok_get<kHashLds>(p, tab, key);
     }
+    // live: some merge of this lane's maps to a key component (value word bit 30); a pass none
+    // of whose merges is live leaves no mergeable pair behind (see scan_tokens_kernel)
+    uint32_t racc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) racc |= r[k] | r[k + 1];
+    uint32_t live = (racc >> 30) & 1u;
     uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
@@ -1669,10 +1691,19 @@ __device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, co
         }
         m[0] = mm;
         st.mv[0] = mm | (vmask << 16);
+        // only the merges that survive the buffer and chunk ends count: look them up again
+        uint32_t lacc = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int h = k >> 1;
+            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
+            if ((mm >> k) & 1u) lacc |= tok_get<kHashLds>(p, tab, key);
+        }
+        live = (lacc >> 30) & 1u;
     } else {
         st.mv[0] = m[0] | 0xFFFF0000u;
     }
-    lane_wave_fns<1>(m, wave, lane, st, wfn);
+    lane_wave_fns<1>(m, wave, lane, st, wfn, __ballot(live) != 0 ? 1u : 0u);
 }
 
 // Emission of a tile's wave range (as emit_tile), its chunk start from the chunk-map word.
@@ -1796,20 +1827,21 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             old = uni(old);
             lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile<kWaves>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                resolve_tile<kWaves, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
             }
         }
 
         if (lbw && Tp < ntiles) {
-            uint32_t C = 1u, how = 0xFFFFu, spins = 0;
+            uint32_t C = 1u, how = 0xFFFFu, spins = 0, live = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
             if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
             wait_ge(p, &s_rdone, it);
-            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
-            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins);
+            const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+            const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
+            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live);
+            live |= (tfl >> 1) & 1u;   // tiles up to and including Tp
             if (lane == 0) {
                 const uint64_t end = O + (C == 1u ? tf3 : tf2);
                 if (C > 1u || O > (uint64_t)Tp * kTileTok || end > n) {
@@ -1820,12 +1852,15 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 s_O[pslot] = O;
                 lds_release(&s_lbdone, it + 1u);
                 const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin));
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
                     *p.total = fin;
                     if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
-                    if (p.done && fin == n) *p.done = 1u;   // merged nothing: the fixpoint
+                    // The fixpoint: this pass merged nothing, or none of its merges made a key
+                    // component, so the next pass merges nothing (a pair of two tokens this pass
+                    // left alone was looked up here and rejected; a new token is in no key).
+                    if (p.done && C <= 1u && (fin == n || !live)) *p.done = p.pass_id;
                 }
                 if (p.debug) {
                     uint64_t* d = p.debug + 4ull * Tp;

@@ -546,3 +546,43 @@ def test_token_scan_device_api_in_place():
         offs = d_off.cpu().numpy()
         assert offs[-1] == tok
         assert np.array_equal(np.diff(offs) * 2, elens)
+
+
+def _u16_passes():
+    return blt_amd._lib.lib().blt_debug_last_u16_passes()
+
+
+def test_token_scan_stops_after_non_live_pass():
+    """The u16 passes end after the first pass none of whose merges made a key component
+    (a component is "live"): the token that pass left alone next to each other were looked up
+    and rejected, and a new token is in no key, so the next pass would merge nothing.  The
+    chained text map stops after one u16 pass; a doubling chain after its depth."""
+    text = synth.text((3 << 20) + 5, seed=31)
+    s = blt_amd.BpeStrategy(CHAINED_TEXT_MAP)
+    for cs in (1 << 20, 65537):
+        got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(CHAINED_TEXT_MAP).run(text, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp) and np.array_equal(lens, elens)
+    assert s.process_chunk(bytes(text[: 1 << 20])) == _oracle_chunk(CHAINED_TEXT_MAP, bytes(text[: 1 << 20]))
+    assert _u16_passes() == 1
+    m = {(97, 97): 256, (256, 256): 257, (257, 257): 258}   # 258 is no component: 2 u16 passes
+    data = b"a" * 65536
+    assert blt_amd.BpeStrategy(m).process_chunk(data) == _oracle_chunk(m, data)
+    assert _u16_passes() == 2
+
+
+def test_token_scan_live_pair_cut_at_chunk_end():
+    """A live pair ("e " -> 256, a key component) cut by a chunk end stays unmerged in every pass
+    and must not keep the chain going: the wave range holding the chunk end looks up only the
+    merges that survive the cut."""
+    cs = 1 << 16
+    text = synth.text(6 * cs + 100, seed=32).copy()
+    for c in range(1, 6):
+        text[c * cs - 1], text[c * cs] = 101, 32   # 'e' | ' ' across every chunk boundary
+    s = blt_amd.BpeStrategy(CHAINED_TEXT_MAP)
+    got = s.process_chunk(bytes(text[:cs]))
+    assert got == _oracle_chunk(CHAINED_TEXT_MAP, bytes(text[:cs]))
+    got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(CHAINED_TEXT_MAP).run(text, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp) and np.array_equal(lens, elens)
+    assert _u16_passes() == 1
