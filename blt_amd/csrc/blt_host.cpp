@@ -612,7 +612,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // once).  u16 pass k runs on the scan kernel while every chunk holds >= kTokRange tokens
     // (a pass at most halves a chunk: chunk_size >> k), else on the generic kernel.  The scan
     // kernel also ends the chain after a pass none of whose merges made a key component, so
-    // most maps finish after one u16 pass: the first batch is 2 passes, later ones 4.  The done
+    // most maps finish after one u16 pass: the first batch is 1 pass, later ones 4.  The done
     // word holds the pass k after which nothing merges; its totals and chunk offsets are [k & 1].
     if (L.nchunks >= (1ull << 32)) return fail(BLT_E_INVALID_INPUT, "too many chunks");
     uint64_t* off[2] = {d_chunk_off ? d_chunk_off : reinterpret_cast<uint64_t*>(ws + L.off_a),
@@ -624,7 +624,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
-    for (int batch = 2;; batch = 4) {
+    for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;

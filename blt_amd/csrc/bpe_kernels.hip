@@ -1126,16 +1126,22 @@ __device__ __forceinline__ void stage_b16(const uint32_t (&v)[8], uint32_t L, ui
 // Copy-out of one stage part: whole 16-byte blocks (at most kCopyBlk per lane) and the head and
 // tail fragments (u16 each, lanes 0..7 and 8..15).
 constexpr int kCopyBlk = (kStageWave + 1023) / 1024;
+// The u16 scan kernel has no 128 KiB table in LDS: its per-wave stage holds a whole wave range's
+// tokens (a 2-byte aligned start and up to 1024 tokens), so every range goes out in one part.
+constexpr int kStageTok = 2064;
+constexpr int kCopyBlkTok = (kStageTok + 1023) / 1024;
 struct CopyPart {
     uint32_t abp;    // 16-byte aligned output byte of the part's first block (from obase)
     uint32_t rgp;    // the part's first token's byte offset from abp (0..15)
     uint32_t re;     // end of the part's tokens, from abp
 };
+template <int NB = kCopyBlk>
 struct CopyData {
-    u32x4 vb[kCopyBlk];
+    u32x4 vb[NB];
     uint16_t vf;
 };
-__device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c, int lane, CopyData& d) {
+template <int NB>
+__device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c, int lane, CopyData<NB>& d) {
     const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
     const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
     const uint32_t nfull = (tbeg - hend) >> 4;
@@ -1143,20 +1149,21 @@ __device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c,
     const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
     const uint8_t* sp = stg;
 #pragma unroll
-    for (int q = 0; q < kCopyBlk; ++q) {
+    for (int q = 0; q < NB; ++q) {
         d.vb[q] = (u32x4){0u, 0u, 0u, 0u};
         if ((uint32_t)lane + 64u * q < nfull) d.vb[q] = *reinterpret_cast<const u32x4*>(sp + hend + 16u * lane + 1024u * q);
     }
     d.vf = bf ? reinterpret_cast<const uint16_t*>(sp)[of >> 1] : (uint16_t)0;
 }
-__device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const CopyPart& c, int lane, const CopyData& d) {
+template <int NB>
+__device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const CopyPart& c, int lane, const CopyData<NB>& d) {
     const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
     const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
     const uint32_t nfull = (tbeg - hend) >> 4;
     const uint32_t of = lane < 8 ? c.rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
     const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
 #pragma unroll
-    for (int q = 0; q < kCopyBlk; ++q)
+    for (int q = 0; q < NB; ++q)
         if ((uint32_t)lane + 64u * q < nfull)
             __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, BLT_STPOL);
     if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, 0);
@@ -1233,7 +1240,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
                 stage_b16(st.v[j], sr[j].L, stg_lds + (gbp & 15u) + 2u * (sr[j].lane_off - base));
             }
             const CopyPart cp = {gbp & ~15u, gbp & 15u, (gbp & 15u) + 2u * cnt};
-            CopyData d;
+            CopyData<> d;
             copy_read(stg, cp, lane, d);
             copy_store(ro, cp, lane, d);
         }
@@ -1302,6 +1309,7 @@ constexpr bool kTiming = false;
 // last (holding back their next phase 1); no priorities at all cost 20 %.
 constexpr int kPrioP1Wave = kWaves / 2, kPrioP1 = 1;
 constexpr int kPrioEmWave = 3 * kWaves / 4, kPrioEm = 2;
+constexpr int kTkTid = 64;   // the lane that claims tickets and hands them over (wave 1)
 __device__ __forceinline__ uint32_t lds_acquire(const uint32_t* f) {
     return __hip_atomic_load(const_cast<uint32_t*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -1394,7 +1402,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // order stays close to publish order (a tile claimed further ahead lands behind
         // later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
-        if (tid == 64 && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
@@ -1490,7 +1498,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         }
         // Tq <- the ticket claimed at this iteration's start (handed over after the claiming
         // wave's emission); T <- Tq (its bytes were loaded during this iteration)
-        if (tid == 64) {
+        if (tid == kTkTid) {
             s_tk[slot] = tk;
             lds_release(&s_tkdone, it + 1u);
         }
@@ -1520,14 +1528,17 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 // pass's structure: tickets, one tile in phase 1 while the previous one is looked back and
 // emitted, barrier-free LDS counters.  The input is the previous pass's big-endian u16 tokens.
 //
-// Geometry: lane l of wave w owns tokens [1024 w + 16 l, +16) of a tile (two 16-byte loads), so a
-// tile is 16 wave ranges of 1024 tokens (32 KiB of input) and has one sub-tile per wave.
+// Geometry: in sub-tile j lane l of wave w owns tokens [16384 j + 1024 w + 16 l, +16) of a tile
+// (two 16-byte loads), so a tile is kSt = 2 sub-tiles of 16 wave ranges of 1024 tokens (64 KiB of
+// input; measured: one sub-tile per tile, 0.65 ms for the 256 MiB multi-pass case against 0.61).
+// A wave range's tokens go out through a per-wave stage that holds all of them (one part).
 //
 // Lookups: a 2-choice cuckoo table of 8-byte buckets [key, value] (the LDS when it fits, else
 // global memory).  The key of the pair (a, b) is the pair's two u16 words as stored, so an even
 // position's key is the lane's input dword itself and an odd one's is one alignbyte; a bucket is
 // the top bits of one v_dot2_u32_u16 of the key with the host's multiplier pair; the value word
-// is BE(v) | 1 << 31, so one byte permute turns two results into the pair's merge mask.
+// is BE(v) | 1 << 31 | live << 30, so one byte permute turns two results into the pair's merge
+// mask, and an OR of the results tells whether a merge made a key component ("live").
 //
 // Chunk ends: the chunk starts of this pass are the previous pass's chunk offsets.
 // chunk_map_kernel turns them into one word per wave range (at most one chunk start and one
@@ -1540,9 +1551,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 // A wave range whose output is its input (no merge before it in the buffer and none in it)
 // writes nothing, so a pass that merges nothing (the fixpoint check) only reads.
 // ===========================================================================================
-constexpr uint32_t kTileTok = (uint32_t)kWaves * kWavePos;
+constexpr int kSt = BLT_TOKS;                              // sub-tiles per token tile
+constexpr uint32_t kSubTok = (uint32_t)kWaves * kWavePos;   // tokens per sub-tile (16 wave ranges)
+constexpr uint32_t kTileTok = (uint32_t)kSt * kSubTok;
+constexpr int kGroupsTok = kSt * kWaves;
 static_assert(kTileTok == kTilePosTok && kWavePos == kTokRange, "token tile geometry");
-static_assert(kS * kWaves <= 64 && kWaves <= 64, "groups");
+static_assert(kGroupsTok <= 64 && kS * kWaves <= 64, "groups");
 
 // Chunk-map word of a wave range: bits 0..10 offset of a chunk start, bit 11 set if there is one;
 // bits 12..22 offset of the last token of a chunk (a start minus one), bit 23 set if there is
@@ -1590,32 +1604,41 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
 }
 
 // Tokens of tile Tn into x (the same straight-line loads as load_tile; near the buffer end the
-// lanes' tokens again one by one), and the wave range's chunk-map word (0 past the end).
+// lanes' tokens again one by one), and each wave range's chunk-map word (0 past the end).
+// Sub-tile j of wave w: tokens [j kSubTok + 1024 w, +1024), wave range Tn kGroupsTok + j kWaves + w.
 __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32_t Tn, uint32_t wave, int lane,
-                                         uint32_t (&x)[8], uint32_t& nxt, uint32_t (&cw)[2]) {
+                                         uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2]) {
     const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
     const uint64_t tile0 = (uint64_t)Tn * kTileTok;
     const uint64_t left = n > tile0 ? n - tile0 : 0;
     const __amdgpu_buffer_rsrc_t rd = rsrc_at(in + 2 * tile0, (2 * left) & ~3ull);
-    const uint32_t wrel = wave * kWavePos;
-    const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
-    const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, BLT_LDPOL);
-    const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, BLT_LDPOL);
-    x[0] = v0[0]; x[1] = v0[1]; x[2] = v0[2]; x[3] = v0[3];
-    x[4] = v1[0]; x[5] = v1[1]; x[6] = v1[2]; x[7] = v1[3];
-    nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, 0);
-    const uint64_t r0 = (uint64_t)Tn * kWaves, nr = (n + kWavePos - 1) / kWavePos;
+    const uint64_t r0 = (uint64_t)Tn * kGroupsTok, nr = (n + kWavePos - 1) / kWavePos;
     const __amdgpu_buffer_rsrc_t rm = rsrc_at(p.cmap + r0, nr > r0 ? 8 * (nr - r0) : 0);
-    const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * wave), 0, 0);
-    cw[0] = c[0]; cw[1] = c[1];
-    const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
-    if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
-        const __amdgpu_buffer_rsrc_t r = rsrc_at(in + 2 * tile0, 2 * left);
-        nxt = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, 0);
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            x[q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, 0) |
-                   ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, 0) << 16);
+    for (int j = 0; j < kSt; ++j) {
+        const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
+        const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
+        const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, BLT_LDPOL);
+        const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, BLT_LDPOL);
+        x[j][0] = v0[0]; x[j][1] = v0[1]; x[j][2] = v0[2]; x[j][3] = v0[3];
+        x[j][4] = v1[0]; x[j][5] = v1[1]; x[j][6] = v1[2]; x[j][7] = v1[3];
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, 0);
+        const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * ((uint32_t)j * kWaves + wave)), 0, 0);
+        cw[j][0] = c[0]; cw[j][1] = c[1];
+    }
+    const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+#pragma unroll
+    for (int j = 0; j < kSt; ++j) {
+        const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
+        if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
+            const __amdgpu_buffer_rsrc_t r = rsrc_at(in + 2 * tile0, 2 * left);
+            const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
+            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, 0);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                x[j][q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, 0) |
+                          ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, 0) << 16);
+        }
     }
 }
 
@@ -1637,14 +1660,16 @@ __device__ __forceinline__ uint32_t tok_get(const PassParams& p, uint32_t tab, u
     return (x[0] == key ? x[1] : 0u) | (y[0] == key ? y[1] : 0u);
 }
 
-// Phase 1 of a wave range of tokens: 16 lookups per lane, the output token of each position if
-// it lands (merged value or the token itself, big-endian, two per register), buffer and chunk
-// ends, then the lane and wave functions (lane_wave_fns).  rn: tokens from the tile start to the
-// buffer end; cwl: low word of the range's chunk-map word.
+// Phase 1 of one wave range of tokens (sub-tile j): 16 lookups per lane, the output token of each
+// position if it lands (merged value or the token itself, big-endian, two per register), buffer
+// and chunk ends; returns the lane's merge mask, sets live when a surviving merge's value is a key
+// component (value word bit 30: a pass with no such merge leaves no mergeable pair behind, see
+// scan_tokens_kernel).  rem: tokens from the range start to the buffer end; cwl: low word of the
+// range's chunk-map word.
 template <bool kHashLds>
-__device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, const uint32_t (&x)[8], uint32_t nxt,
-                                           uint32_t rn, uint32_t cwl, uint32_t wave, int lane, TileStateT<1>& st,
-                                           uint32_t (*wfn)[4]) {
+__device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab, const uint32_t (&x)[8],
+                                               uint32_t nxt, uint32_t rem, uint32_t cwl, int lane, int j,
+                                               TileStateT<kSt>& st, uint32_t& live) {
     // next lane's first token (wave_shl:1); lane 63 keeps the token after the wave's range
     const uint32_t nbw = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false);
     uint32_t r[16];
@@ -1654,28 +1679,24 @@ __device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, co
         const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
         r[k] = tok_get<kHashLds>(p, tab, key);
     }
-    // live: some merge of this lane's maps to a key component (value word bit 30); a pass none
-    // of whose merges is live leaves no mergeable pair behind (see scan_tokens_kernel)
     uint32_t racc = 0;
 #pragma unroll
     for (int k = 0; k < 16; k += 2) racc |= r[k] | r[k + 1];
-    uint32_t live = (racc >> 30) & 1u;
+    uint32_t lv = (racc >> 30) & 1u;
     uint32_t m32 = 0;   // even positions in bits 0..14, odd positions in bits 16..30
 #pragma unroll
     for (int h = 0; h < 8; ++h) {
         const uint32_t R = __builtin_amdgcn_perm(r[2 * h + 1], r[2 * h], 0x05040100u);     // both values
         const uint32_t hit = __builtin_amdgcn_perm(r[2 * h + 1], r[2 * h], 0x0B0B0909u);   // bit 31 -> half
-        st.v[0][h] = (hit & R) | (~hit & x[h]);
+        st.v[j][h] = (hit & R) | (~hit & x[h]);
         m32 |= (hit & 0x00010001u) << (2 * h);
     }
-    uint32_t m[1] = {(m32 & 0xFFFFu) | (m32 >> 15)};
-    const uint32_t wrel = wave * kWavePos;
-    const uint32_t rem = rn > wrel ? rn - wrel : 0u;
+    uint32_t m = (m32 & 0xFFFFu) | (m32 >> 15);
     const bool has_end = (cwl & kCmEnd) != 0u;
     if (rem <= kWavePos || has_end) {   // uniform; rare
         const int32_t rr = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
-        uint32_t mm = m[0] & ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u));
+        uint32_t mm = m & ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u));
         uint32_t forced = (rr >= 1 && rr <= 16) ? (1u << (rr - 1)) : 0u;   // the buffer's last token
         if (has_end) {                                                     // a chunk's last token
             const uint32_t e = ((cwl >> 12) & 0x7FFu) - 16u * (uint32_t)lane;
@@ -1686,11 +1707,11 @@ __device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, co
             for (int h = 0; h < 8; ++h) {
                 const uint32_t fm = (((forced >> (2 * h)) & 1u) ? 0x0000FFFFu : 0u) |
                                     (((forced >> (2 * h + 1)) & 1u) ? 0xFFFF0000u : 0u);
-                st.v[0][h] = (st.v[0][h] & ~fm) | (x[h] & fm);
+                st.v[j][h] = (st.v[j][h] & ~fm) | (x[h] & fm);
             }
         }
-        m[0] = mm;
-        st.mv[0] = mm | (vmask << 16);
+        m = mm;
+        st.mv[j] = mm | (vmask << 16);
         // only the merges that survive the buffer and chunk ends count: look them up again
         uint32_t lacc = 0;
 #pragma unroll
@@ -1699,35 +1720,36 @@ __device__ __forceinline__ void phase1_tok(const PassParams& p, uint32_t tab, co
             const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
             if ((mm >> k) & 1u) lacc |= tok_get<kHashLds>(p, tab, key);
         }
-        live = (lacc >> 30) & 1u;
+        lv = (lacc >> 30) & 1u;
     } else {
-        st.mv[0] = m[0] | 0xFFFF0000u;
+        st.mv[j] = m | 0xFFFF0000u;
     }
-    lane_wave_fns<1>(m, wave, lane, st, wfn, __ballot(live) != 0 ? 1u : 0u);
+    live |= lv;
+    return m;
 }
 
-// Emission of a tile's wave range (as emit_tile), its chunk start from the chunk-map word.
-__device__ __forceinline__ void emit_tok(const PassParams& p, uint32_t Tp, uint32_t rn, uint32_t cwl, uint32_t cwh,
-                                         uint32_t wave, int lane, const TileStateT<1>& st, const uint32_t (*gin)[4],
+// Emission of sub-tile j's wave range (as emit_tile), its chunk start from the chunk-map word.
+// rem: tokens from the range start to the buffer end; wtok: the range's first input token.
+__device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uint32_t rem, uint32_t cwl, uint32_t cwh,
+                                         int lane, int j, const TileStateT<kSt>& st, const uint32_t* gin,
                                          uint32_t C, uint64_t O, uint8_t* stg) {
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
     const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
-    const uint32_t wrel = wave * kWavePos;
-    const uint32_t cg = uni(gin[wave][C]);
-    const uint32_t goff = uni(gin[wave][2 + C]);   // tokens before this wave range in the tile
-    const uint32_t gb = orel + 2u * goff;          // output byte of the wave range, from obase
+    const uint32_t cg = uni(gin[C]);
+    const uint32_t goff = uni(gin[2 + C]);   // tokens before this wave range in the tile
+    const uint32_t gb = orel + 2u * goff;    // output byte of the wave range, from obase
     const bool cstart = p.chunk_off && (cwl & kCmStart) != 0u;
-    if (__ballot(st.mv[0] != 0xFFFFFFFFu) == 0) {
+    if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
         // dense: every pair merges, so the only possible chunk start is the range's first token
         if (cstart && lane == 0) p.chunk_off[cwh] = O + goff;
-        emit_dense(st.v[0], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
+        emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
     }
-    const uint32_t m = st.mv[0] & 0xFFFFu, vmask = st.mv[0] >> 16;
-    const uint32_t c = __builtin_amdgcn_ubfe(st.lw[0], cg, 1);
-    const uint32_t lane_off = cg ? (st.ex[0] >> 16) : (st.ex[0] & 0xFFFFu);
+    const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
+    const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
+    const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
     const uint32_t mc = c ? m : (m & ~1u);
     const uint32_t sst = mc & ~(mc << 1);
     const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
@@ -1739,29 +1761,21 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint32_t Tp, uint3
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
-    const uint32_t rem = rn > wrel ? (rn - wrel < kWavePos ? rn - wrel : kWavePos) : 0u;
-    if (wcnt == rem && O + goff == (uint64_t)Tp * kTileTok + wrel) return;
-    const uint32_t two = (gb & 15u) + 2u * wcnt <= (uint32_t)kStageWave ? 0u : 1u;
-    const uint32_t off32 = two ? uni(lane_u32(lane_off, 32)) : 0u;   // tokens before lane 32
-    const uint32_t stg_lds = lds_addr(stg);
-    for (uint32_t part = 0; part <= two; ++part) {
-        const uint32_t base = part ? off32 : 0u;
-        const uint32_t cnt = two ? (part ? wcnt - off32 : off32) : wcnt;
-        const uint32_t gbp = gb + 2u * base;
-        if (!two || ((uint32_t)lane >> 5) == part) stage_b16(st.v[0], L, stg_lds + (gbp & 15u) + 2u * (lane_off - base));
-        const CopyPart cp = {gbp & ~15u, gbp & 15u, (gbp & 15u) + 2u * cnt};
-        CopyData d;
-        copy_read(stg, cp, lane, d);
-        copy_store(ro, cp, lane, d);
-    }
+    if (wcnt == (rem < kWavePos ? rem : kWavePos) && O + goff == wtok) return;
+    // one part: the stage holds the range's at most 1024 tokens
+    stage_b16(st.v[j], L, lds_addr(stg) + (gb & 15u) + 2u * lane_off);
+    const CopyPart cp = {gb & ~15u, gb & 15u, (gb & 15u) + 2u * wcnt};
+    CopyData<kCopyBlkTok> d;
+    copy_read(stg, cp, lane, d);
+    copy_store(ro, cp, lane, d);
 }
 
 template <bool kHashLds>
 __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
-    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kWaves][4];
-    __shared__ uint32_t s_gin[kRing][kWaves][4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageTok];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroupsTok][4];
+    __shared__ uint32_t s_gin[kRing][kGroupsTok][4];
     __shared__ uint32_t s_tfn[kRing][4];
     __shared__ uint64_t s_O[kRing];
     __shared__ uint32_t s_C[kRing];
@@ -1775,8 +1789,10 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     const uint32_t wave = uni((uint32_t)tid >> 6);
     const uint64_t n = uni64(token_count(p));
     const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
-    auto rn_of = [&](uint32_t T) {
-        const uint64_t l = n - (uint64_t)T * kTileTok;
+    // tokens from sub-tile j's wave range start of tile T to the buffer end (clamped)
+    auto rem_of = [&](uint32_t T, int j) {
+        const uint64_t w0 = (uint64_t)T * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
+        const uint64_t l = n > w0 ? n - w0 : 0;
         return (uint32_t)(l > 0x7FFFFFFFull ? 0x7FFFFFFFull : l);
     };
 
@@ -1799,27 +1815,41 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     __syncthreads();
 
-    uint32_t xa[8], xb[8], na = 0, nb = 0, ca[2] = {0u, 0u}, cb[2] = {0u, 0u};
+    uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca[kSt][2], cb[kSt][2];
+#pragma unroll
+    for (int j = 0; j < kSt; ++j) { na[j] = nb[j] = 0u; ca[j][0] = ca[j][1] = cb[j][0] = cb[j][1] = 0u; }
     if (T < ntiles) load_tok(p, n, T, wave, lane, xa, na, ca);
-    TileStateT<1> sa, sb;
+    TileStateT<kSt> sa, sb;
     uint64_t lbs[kLbWin];
     uint32_t it = 0;
-    uint32_t cwpl = 0, cwph = 0;   // Tp's chunk-map word
+    uint32_t cwp[kSt][2];   // Tp's chunk-map words
+#pragma unroll
+    for (int j = 0; j < kSt; ++j) cwp[j][0] = cwp[j][1] = 0u;
 
-    auto step = [&](uint32_t (&x)[8], uint32_t& nxt, uint32_t (&cw)[2], uint32_t (&xq)[8], uint32_t& nxtq,
-                    uint32_t (&cwq)[2], TileStateT<1>& sc, const TileStateT<1>& sp) {
+    auto step = [&](uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2], uint32_t (&xq)[kSt][8],
+                    uint32_t (&nxtq)[kSt], uint32_t (&cwq)[kSt][2], TileStateT<kSt>& sc, const TileStateT<kSt>& sp) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map word have landed
-        const uint32_t cwl = uni(cw[0]), cwh = uni(cw[1]);
+        uint64_t stamp[7];
+        const bool stamping = kTiming && p.debug != nullptr;
+        if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map words have landed
+        if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
+        uint32_t cwl[kSt], cwh[kSt];
+#pragma unroll
+        for (int j = 0; j < kSt; ++j) { cwl[j] = uni(cw[j][0]); cwh[j] = uni(cw[j][1]); }
         if (Tq < ntiles) load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
         uint32_t tk = kNone;
-        if (tid == 64 && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
+        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
         bool lbw = wave == 0;
         if (T < ntiles) {
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tok<kHashLds>(p, tab, x, nxt, rn_of(T), cwl, wave, lane, sc, s_wfn[slot]);
+            uint32_t m[kSt], live = 0;
+#pragma unroll
+            for (int j = 0; j < kSt; ++j)
+                m[j] = phase1_tok<kHashLds>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
+            lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], __ballot(live) != 0 ? 1u : 0u);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
@@ -1827,10 +1857,11 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             old = uni(old);
             lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile<kWaves, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                resolve_tile<kGroupsTok, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
             }
         }
+        if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
 
         if (lbw && Tp < ntiles) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, live = 0;
@@ -1872,16 +1903,25 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             }
         }
 
+        if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
         if (Tp < ntiles) {
             wait_ge(p, &s_lbdone, it + 1u);
+            if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
             const uint32_t Cp = uni(s_C[pslot]);
-            if (Cp <= 1u)
-                emit_tok(p, Tp, rn_of(Tp), cwpl, cwph, wave, lane, sp, s_gin[pslot], Cp, uni64(s_O[pslot]),
-                         s_stage[wave]);
+            if (Cp <= 1u) {
+                const uint64_t Op = uni64(s_O[pslot]);
+#pragma unroll
+                for (int j = 0; j < kSt; ++j) {
+                    const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
+                    emit_tok(p, wtok, rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
+                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage[wave]);
+                }
+            }
             __builtin_amdgcn_s_setprio(0);
         }
-        if (tid == 64) {
+        if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
+        if (tid == kTkTid) {
             s_tk[slot] = tk;
             lds_release(&s_tkdone, it + 1u);
         }
@@ -1891,8 +1931,14 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             Tr = uni(s_tk[slot]);
             if (Tr >= ntiles) Tr = kNone;
         }
-        cwpl = cwl;
-        cwph = cwh;
+        if (stamping && Tp < ntiles && lane == 0) {
+            stamp[6] = __builtin_amdgcn_s_memtime();
+            uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
+        }
+#pragma unroll
+        for (int j = 0; j < kSt; ++j) { cwp[j][0] = cwl[j]; cwp[j][1] = cwh[j]; }
         Tp = T;
         T = Tq;
         Tq = Tr;

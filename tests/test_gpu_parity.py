@@ -449,7 +449,8 @@ def test_concurrent_full_size_chunks():
 
 
 # ---- u16 passes of general maps on the token scan kernel (seg::scan_tokens_kernel) ----------
-TOK_TILE = 16384  # tokens per tile of the token scan kernel (bpe_kernels.h kTilePosTok)
+TOK_TILE = 32768  # tokens per tile of the token scan kernel (bpe_kernels.h kTilePosTok)
+TOK_SUB = 16384   # tokens per sub-tile (16 wave ranges of 1024)
 CHAINED_TEXT_MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259,
                     (259, 104): 260}
 
@@ -466,10 +467,11 @@ def test_token_scan_chunk_geometry(cs):
     assert np.array_equal(lens, elens)
 
 
-@pytest.mark.parametrize("n", [1023, 1024, 1025, 2 * 1024 + 17, TOK_TILE - 1, TOK_TILE, TOK_TILE + 1,
+@pytest.mark.parametrize("n", [1023, 1024, 1025, 2 * 1024 + 17, TOK_SUB - 1, TOK_SUB, TOK_SUB + 1,
+                               TOK_TILE - 1, TOK_TILE, TOK_TILE + 1, TOK_TILE + TOK_SUB + 3,
                                2 * TOK_TILE + 16, 5 * TOK_TILE + 1000, 40 * TOK_TILE + 3])
 def test_token_scan_buffer_ends(n):
-    """Token counts around wave-range (1024) and tile (16384) edges: "aa" -> 256 on pass 1 and
+    """Token counts around wave-range (1024), sub-tile (16384) and tile (32768) edges: "aa" -> 256 on pass 1 and
     (256, 256) -> 257, (257, 257) -> 258 on the u16 passes, with a lone byte at every tenth slot."""
     rng = np.random.default_rng(n)
     data = np.full(2 * n + 1, 97, np.uint8)
