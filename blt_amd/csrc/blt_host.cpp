@@ -259,6 +259,7 @@ struct blt_bpe {
     // | 1 << 30 when the value is a component of some key.
     std::vector<uint32_t> hwords;
     uint32_t hmul1 = 0, hmul2 = 0, hshift = 0;
+    bool hone = false;                     // one-probe table (hmul2 == hmul1)
     DevTables dev[kMaxDevices];
     // Sticky device-error word in pinned, mapped host memory: any kernel of this handle that flags
     // an error (look-back timeout, output range, prefix invariant) stores 1 here, and every later
@@ -295,6 +296,32 @@ bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, const std:
         seed = seed * 6364136223846793005ull + 1442695040888963407ull;
         return (uint32_t)(seed >> 32) | 0x00010001u;   // two odd 16-bit multipliers
     };
+    // Small maps first try a one-probe table (every key in its own bucket of one hash), up to
+    // 4096 buckets (32 KiB of LDS): the u16 scan kernel then reads one bucket per lookup.
+    for (uint32_t l2 = log2nb; keys.size() <= 512 && l2 <= 12; ++l2) {
+        const uint32_t nb = 1u << l2, shift = 32 - l2;
+        for (int attempt = 0; attempt < 64; ++attempt) {
+            const uint32_t m1 = next_mul();
+            std::vector<uint32_t> key(nb, empty), val(nb, 0);
+            bool ok = true;
+            for (size_t i = 0; i < keys.size() && ok; ++i) {
+                const uint32_t b = blt::bucket_of(keys[i], m1, shift);
+                ok = key[b] == empty;
+                key[b] = keys[i];
+                val[b] = vals[i];
+            }
+            if (!ok) continue;
+            h->hwords.assign(2ull * nb, 0);
+            for (uint32_t i = 0; i < nb; ++i) {
+                h->hwords[2 * i] = key[i];
+                h->hwords[2 * i + 1] = val[i];
+            }
+            h->hmul1 = h->hmul2 = m1;
+            h->hshift = shift;
+            h->hone = true;
+            return true;
+        }
+    }
     for (; log2nb <= 25; ++log2nb) {
         const uint32_t nb = 1u << log2nb, shift = 32 - log2nb;
         for (int attempt = 0; attempt < 32; ++attempt) {
@@ -557,6 +584,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.hmul2 = h->hmul2;
     p.hshift = h->hshift;
     p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
+    p.hone = h->hone ? 1u : 0u;
     p.cs_magic = cs ? ~0ull / cs : 0;
     if (cs && cs % blt::kTilePosBytes == 0 && cs / blt::kTilePosBytes < (1ull << 31)) {
         p.cs_tiles = (uint32_t)(cs / blt::kTilePosBytes);

@@ -43,6 +43,8 @@ struct PassParams {
     uint32_t hmul1, hmul2;     // bucket of key: dot2(key, hmul) >> hshift (u16 halves), two choices
     uint32_t hshift;
     uint32_t hbytes;           // table bytes (u16 passes stage the table in LDS when it fits)
+    uint32_t hone;             // the table is one-probe: every key sits in bucket dot2(key, hmul1) >> hshift
+                               // (hmul2 == hmul1, so two-probe readers stay correct)
     const uint64_t* n_dev;     // u16 passes: the token count written by the previous pass (on device)
     uint32_t* done;            // u16 passes: set to pass_id by the pass after which the next merges
                                // nothing (it merged nothing, or none of its merges made a key

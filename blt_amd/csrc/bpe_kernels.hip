@@ -1642,14 +1642,21 @@ __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32
     }
 }
 
-// Lookup of one pair key in the token table: LDS byte address tab (kHashLds) or global memory.
-template <bool kHashLds>
+// Lookup of one pair key in the token table.  kHash: 0 the 2-choice table in global memory (L2),
+// 1 the 2-choice table in LDS (byte address tab), 2 a one-probe table in LDS (small maps: the host
+// found a multiplier that puts every key in its own bucket).
+template <int kHash>
 __device__ __forceinline__ uint32_t tok_get(const PassParams& p, uint32_t tab, uint32_t key) {
-    const uint32_t b1 = bucket_hash(key, p.hmul1, p.hshift), b2 = bucket_hash(key, p.hmul2, p.hshift);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+    const uint32_t b1 = bucket_hash(key, p.hmul1, p.hshift);
+    if constexpr (kHash == 2) {
+        const u32x2 x = *(const lds_u32x2*)(uintptr_t)(tab + 8u * b1);
+        return x[0] == key ? x[1] : 0u;
+    }
+    const uint32_t b2 = bucket_hash(key, p.hmul2, p.hshift);
     u32x2 x, y;
-    if constexpr (kHashLds) {
-        typedef __attribute__((address_space(3))) u32x2 lds_u32x2;
+    if constexpr (kHash == 1) {
         x = *(const lds_u32x2*)(uintptr_t)(tab + 8u * b1);
         y = *(const lds_u32x2*)(uintptr_t)(tab + 8u * b2);
     } else {
@@ -1666,7 +1673,7 @@ __device__ __forceinline__ uint32_t tok_get(const PassParams& p, uint32_t tab, u
 // component (value word bit 30: a pass with no such merge leaves no mergeable pair behind, see
 // scan_tokens_kernel).  rem: tokens from the range start to the buffer end; cwl: low word of the
 // range's chunk-map word.
-template <bool kHashLds>
+template <int kHash>
 __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab, const uint32_t (&x)[8],
                                                uint32_t nxt, uint32_t rem, uint32_t cwl, int lane, int j,
                                                TileStateT<kSt>& st, uint32_t& live) {
@@ -1677,7 +1684,7 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
     for (int k = 0; k < 16; ++k) {
         const int h = k >> 1;
         const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
-        r[k] = tok_get<kHashLds>(p, tab, key);
+        r[k] = tok_get<kHash>(p, tab, key);
     }
     uint32_t racc = 0;
 #pragma unroll
@@ -1718,7 +1725,7 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
         for (int k = 0; k < 16; ++k) {
             const int h = k >> 1;
             const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
-            if ((mm >> k) & 1u) lacc |= tok_get<kHashLds>(p, tab, key);
+            if ((mm >> k) & 1u) lacc |= tok_get<kHash>(p, tab, key);
         }
         lv = (lacc >> 30) & 1u;
     } else {
@@ -1770,8 +1777,9 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     copy_store(ro, cp, lane, d);
 }
 
-template <bool kHashLds>
+template <int kHash>
 __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
+    constexpr bool kHashLds = kHash != 0;
     extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageTok];
     __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroupsTok][4];
@@ -1848,7 +1856,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             uint32_t m[kSt], live = 0;
 #pragma unroll
             for (int j = 0; j < kSt; ++j)
-                m[j] = phase1_tok<kHashLds>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
+                m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
             lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], __ballot(live) != 0 ? 1u : 0u);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
@@ -2022,7 +2030,7 @@ __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
 // per (device, kernel) and cached in atomics (launchers run concurrently from many host threads).
 struct GridCache {
     std::atomic<int> cus[64];
-    std::atomic<int> occ[64][6];
+    std::atomic<int> occ[64][8];
 };
 static GridCache g_grid;   // zero-initialised (static storage)
 static int grid_for(uint32_t ntiles, int device, const void* fn, int threads, int kernel_id) {
@@ -2094,12 +2102,16 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
     const uint64_t ranges = (p.n + kTokRange - 1) / kTokRange;
     hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
     const bool lds = p.hbytes <= kHashLdsMax;
-    const void* fn = lds ? (const void*)seg::scan_tokens_kernel<true> : (const void*)seg::scan_tokens_kernel<false>;
+    const int mode = lds ? (p.hone ? 2 : 1) : 0;
+    const void* fn = mode == 2 ? (const void*)seg::scan_tokens_kernel<2>
+                     : mode == 1 ? (const void*)seg::scan_tokens_kernel<1> : (const void*)seg::scan_tokens_kernel<0>;
     const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
-    const int grid = grid_for(ntiles, device, fn, seg::kThreads, lds ? 2 : 3);
+    const int grid = grid_for(ntiles, device, fn, seg::kThreads, 5 + mode);
     const size_t smem = lds ? p.hbytes : 0;
-    if (lds) hipLaunchKernelGGL((seg::scan_tokens_kernel<true>), dim3((unsigned)grid), dim3(seg::kThreads), smem, s, p);
-    else hipLaunchKernelGGL((seg::scan_tokens_kernel<false>), dim3((unsigned)grid), dim3(seg::kThreads), 0, s, p);
+    const dim3 g((unsigned)grid), b(seg::kThreads);
+    if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2>), g, b, smem, s, p);
+    else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1>), g, b, smem, s, p);
+    else hipLaunchKernelGGL((seg::scan_tokens_kernel<0>), g, b, 0, s, p);
     return hipGetLastError();
 }
 

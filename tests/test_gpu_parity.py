@@ -588,3 +588,23 @@ def test_token_scan_live_pair_cut_at_chunk_end():
     exp, elens = O.COracle(CHAINED_TEXT_MAP).run(text, cs, threads=8, return_lens=True)
     assert np.array_equal(got, exp) and np.array_equal(lens, elens)
     assert _u16_passes() == 1
+
+
+def test_token_scan_lds_two_choice_table():
+    """A general map of ~1000 keys: too many for the one-probe table (small maps), small enough
+    for the 2-choice table in LDS."""
+    letters = range(97, 123)
+    m = {}
+    for i, (a, b) in enumerate((a, b) for a in letters for b in letters):
+        m[(a, b)] = 256 + i
+    for i in range(0, 676, 2):
+        m[(256 + i, 97 + i % 26)] = 2000 + i
+    assert 512 < len(m) < 3072
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    rng = np.random.default_rng(5)
+    data = rng.integers(97, 123, (3 << 20) + 11, dtype=np.uint8)
+    got, lens = s.process_chunks(data, 1 << 20, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, 1 << 20, threads=8, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(lens, elens)
