@@ -21,7 +21,8 @@ version beside it.
 At N = 1 the line also carries (rank 0, outside the timed region of `value`):
   * `configs`: the other BASELINE workloads on the same kernel, device-resident, kernel-only
     (median of HIP-event timings), each with its roofline fraction and a bit-exact check:
-    cfg2 (100 MiB text, 256 merges) and cfg5 (1 GiB random bytes, cfg3's 50k merges);
+    cfg2 (100 MiB text, 256 merges) and cfg5 (1 GiB random bytes, cfg3's 50k merges); `multi`:
+    the f2 general map (256 MiB text, chained merges: one byte pass and u16 passes);
   * `end_to_end`: cfg3 through blt_bpe_process_chunks from pageable host memory (PCIe-inclusive);
   * `per_chunk_path`: 16 host threads calling blt_bpe_process_chunk on the 64 16-MiB chunks of
     cfg3 (the reference's per-chunk strategy calls, pipeline.rs:86, :141-150).
@@ -124,7 +125,48 @@ def extra_configs(blt_amd, synth, O, threads):
                      "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
         del d_in, d_out
         s.close()
+    res["multi"] = general_map_rate(blt_amd, synth, O, threads)
     return res
+
+
+# f2: a general map that needs more than one pass (chained and byte-valued merges, SURVEY.md §8a
+# row f2): one byte pass, then u16 passes until the chain provably stops.
+MULTI_MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
+
+
+def general_map_rate(blt_amd, synth, O, threads, reps=10):
+    """256 MiB of cfg2's text through the chained map, device-resident; the timed region is the
+    whole encode_device call (byte pass, u16 passes, the host's read of the pass count)."""
+    import torch
+    host = synth.text(256 << 20, seed=2)
+    n = host.size
+    s = blt_amd.BpeStrategy(MULTI_MAP)
+    d_in = torch.from_numpy(host).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    wsb = s.workspace_size(n, CHUNK)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    tok = s.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        s.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=False)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = float(np.median(ts))
+    passes = int(blt_amd._lib.lib().blt_debug_last_u16_passes())
+    got = d_out[:2 * tok].cpu().numpy()
+    exp = O.COracle(MULTI_MAP).run(host, CHUNK, threads=threads)
+    algo = n + 2 * tok
+    s.close()
+    return {"workload": "f2: 256 MiB synthetic text (cfg2's), chained + byte-valued 6-entry map, --chunksize 16MB",
+            "bytes": n, "ms": round(ms, 4), "u16_passes": passes, "input_GBps": round(n / ms / 1e6, 1),
+            "achieved_GBps": round(algo / ms / 1e6, 1), "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "tokens_per_byte": round(tok / n, 4),
+            "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
 
 
 def host_paths(blt_amd, strategy, host, exp):
