@@ -43,6 +43,8 @@ def main():
             mib = int(cfg[4:])
             host = synth.text(mib << 20, seed=2)
             merges = synth.merges_dict(synth.top_pair_merges(synth.text(100 << 20, seed=2), 256))
+        elif cfg == "same":   # --mib of one repeated byte under cfg3's merges: dense, every lookup one LDS entry
+            host, merges = np.full(n, 101, np.uint8), m3
         elif cfg == "cfg2big":   # cfg2's text and merges at the --mib size: steady-state cost per tile
             host = synth.text(n, seed=2)
             merges = synth.merges_dict(synth.top_pair_merges(host[: 100 << 20], 256))
