@@ -801,7 +801,7 @@ __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t 
 template <bool kBE, bool kHiM>
 __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS][4], const uint32_t (&nxt)[kS],
                                             const TInfo& ti, uint32_t cs32, uint32_t wave, int lane,
-                                            TileState& st, uint32_t (*wfn)[4]) {
+                                            TileState& st, uint32_t (*wfn)[4], uint64_t* sub = nullptr) {
     uint32_t m[kS];
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
@@ -879,7 +879,15 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             st.mv[j] = m[j] | 0xFFFF0000u;
         }
     }
+    if (sub) {   // timing build: lookups and masks done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        sub[0] = __builtin_amdgcn_s_memtime();
+    }
     lane_wave_fns<kS>(m, wave, lane, st, wfn);
+    if (sub) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        sub[1] = __builtin_amdgcn_s_memtime();
+    }
 }
 
 // ---- tile resolve (one wave): group carries and offsets, tile function, publish -------------
@@ -1392,7 +1400,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     auto step = [&](uint32_t (&x)[kS][4], uint32_t (&nxt)[kS], uint32_t (&xq)[kS][4], uint32_t (&nxtq)[kS],
                     TileState& sc, const TileState& sp) {
         const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
-        uint64_t stamp[7];
+        uint64_t stamp[7], sub[2] = {0, 0};
         const bool stamping = kTiming && p.debug != nullptr;
         if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's bytes have landed
@@ -1412,7 +1420,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot]);
+            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot], stamping ? sub : nullptr);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
@@ -1491,6 +1499,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
 #pragma unroll
             for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
+            w[6] = sub[0] ? sub[0] - stamp[1] : 0;   // phase 1 split: lookups and masks | lane functions
+            w[7] = sub[0] ? sub[1] - sub[0] : 0;
         }
         if (stamping && tid == 0 && Tp < ntiles) {
             uint64_t* e = p.debug + 4ull * ntiles + 4ull * Tp;

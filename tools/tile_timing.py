@@ -45,14 +45,18 @@ def main():
     L.blt_debug_set_tile_record(None)
     rec = dbg.cpu().numpy().astype(np.int64)
     how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
-    wv = rec[8 * ntiles:].reshape(ntiles, 16, 8)[:, :, :6]
+    wv8 = rec[8 * ntiles:].reshape(ntiles, 16, 8)
+    wv = wv8[:, :, :6]
     ok = wv[:, 0, :].sum(axis=1) > 0
     wv = wv[ok]
+    sub = wv8[ok][:, :, 6:8]
     names = ["x-wait", "phase1", "lb+pub", "lb-wait", "emit", "tk-wait"]
     print("per wave mean cycles: " + " ".join(f"{x:>8s}" for x in names) + "     total")
     for w in range(16):
         m = wv[:, w, :].mean(axis=0)
         print(f"  wave {w:2d}:          " + " ".join(f"{v:8.0f}" for v in m) + f"  {m.sum():8.0f}")
+    print("phase 1 split (lookups+masks | lane functions, lgkmcnt drained): " +
+          " ".join(f"w{w}:{sub[:, w, 0].mean():.0f}|{sub[:, w, 1].mean():.0f}" for w in range(16)))
     sp = rec[4 * ntiles + 3:8 * ntiles:4] & 0xFFFFFFFF
     bad = rec[4 * ntiles + 3:8 * ntiles:4] >> 32
     print(f"look-back spins mean {sp.mean():.2f} max {sp.max()}")
