@@ -14,7 +14,7 @@ ORACLE := oracle/liboracle.so
 CLI := blt_amd/blt
 OBJDIR := build
 
-all: $(LIB) $(SYNTH) $(ORACLE) $(CLI)
+all: $(LIB) $(SYNTH) $(ORACLE) $(CLI) sanitize
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)
@@ -51,3 +51,26 @@ clean:
 timing:
 	bash tools/build_variant.sh timing -DBLT_TIMING
 .PHONY: timing
+
+# Host-sanitizer build (test infrastructure): the library's host code with ASan and
+# UBSan (device code untouched), linked into tests/native/sanitize_driver.cpp with the C oracle as
+# the checker.  `build/san/blt_sanitize_driver --cpu` runs the host-only checks (no GPU needed).
+SANFLAGS := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
+            -Xarch_host -fno-sanitize-recover=undefined
+SAN := build/san
+# one compiler for every instrumented object (one sanitizer runtime)
+SANCC := /opt/rocm/lib/llvm/bin/clang
+sanitize: $(SAN)/blt_sanitize_driver
+$(SAN):
+	mkdir -p $(SAN)
+$(SAN)/blt_host.o: blt_amd/csrc/blt_host.cpp blt_amd/csrc/bpe_kernels.h include/blt_bpe.h | $(SAN)
+	$(HIPCC) $(HIPFLAGS) -O1 $(SANFLAGS) -x hip -c $< -o $@
+$(SAN)/blt_pipeline.o: blt_amd/csrc/blt_pipeline.cpp include/blt_bpe.h | $(SAN)
+	$(HIPCC) $(HIPFLAGS) -O1 $(SANFLAGS) -x hip -c $< -o $@
+$(SAN)/oracle.o: oracle/bpe_oracle.c | $(SAN)
+	$(SANCC) -O1 -g -fPIC -std=c11 -pthread -fsanitize=address,undefined -fno-omit-frame-pointer -c $< -o $@
+$(SAN)/driver.o: tests/native/sanitize_driver.cpp include/blt_bpe.h | $(SAN)
+	$(SANCC)++ -O1 -g -std=c++17 -pthread -fsanitize=address,undefined -fno-omit-frame-pointer -c $< -o $@
+$(SAN)/blt_sanitize_driver: $(SAN)/driver.o $(OBJDIR)/bpe_kernels.o $(SAN)/blt_host.o $(SAN)/blt_pipeline.o $(SAN)/oracle.o
+	$(HIPCC) -fno-gpu-sanitize -fsanitize=address,undefined -o $@ $^ -lpthread
+.PHONY: sanitize

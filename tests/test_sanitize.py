@@ -1,0 +1,36 @@
+"""The C ABI's host code under AddressSanitizer and UndefinedBehaviorSanitizer.
+
+`make sanitize` builds tests/native/sanitize_driver.cpp against the library's host objects
+compiled with -Xarch_host -fsanitize=address,undefined (device code untouched) and the C oracle as
+the checker.  Host-only checks run here; with a GPU the driver also checks process_chunk,
+process_chunks, the basic strategy and run_tokenizer against the oracle, with 8 threads sharing a
+handle.  Any sanitizer report aborts the driver (non-zero exit).
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "build", "san", "blt_sanitize_driver")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+
+
+def _driver():
+    if not os.path.exists(DRIVER):
+        subprocess.run(["make", "-C", ROOT, "-j8", "sanitize"], check=True, capture_output=True)
+    return DRIVER
+
+
+def test_host_checks_under_asan_ubsan():
+    r = subprocess.run([_driver(), "--cpu"], capture_output=True, text=True, env=ENV, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host checks: 0 failure(s)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_device_checks_under_asan_ubsan():
+    r = subprocess.run([_driver()], capture_output=True, text=True, env=ENV, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "host and device checks: 0 failure(s)" in r.stdout, r.stdout
