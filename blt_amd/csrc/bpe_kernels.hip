@@ -700,8 +700,8 @@ template <int NS>
 struct TileStateT {
     uint32_t v[NS][8];   // looked-up tokens, two per register
     uint32_t mv[NS];     // merge mask | valid mask << 16
-    uint32_t lw[NS];     // carry-in for wave carry-in 0 | for wave carry-in 1 << 1
-    uint32_t ex[NS];     // exclusive prefix count, carry-in 0 | carry-in 1 << 16
+    uint32_t ex[NS];     // per wave carry-in h (h = 0: bits 0..15, h = 1: bits 16..31): the lane's
+                         // exclusive prefix count (bits 0..14) and its carry-in (bit 15)
 };
 using TileState = TileStateT<kS>;
 
@@ -777,8 +777,7 @@ __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t 
         // per lane: count under its carry-in, for wave carry-in 0 (low half) and 1 (high half)
         const uint32_t packed = lane_sel(CI0, cnt0, cnt1) | (lane_sel(CI1, cnt0, cnt1) << 16);
         const uint32_t incl = wave_scan(packed);
-        st.ex[j] = incl - packed;
-        st.lw[j] = lane_sel(CI0, 0u, 1u) | lane_sel(CI1, 0u, 2u);   // carry-in for wave carry-in 0 | 1 << 1
+        st.ex[j] = (incl - packed) | lane_sel(CI0, 0u, 0x8000u) | lane_sel(CI1, 0u, 0x80000000u);
         wcmask[j] = cmask;
         wincl[j] = incl;
     }
@@ -1216,8 +1215,8 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
             continue;
         }
         const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
-        const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
-        const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
+        const uint32_t c = __builtin_amdgcn_ubfe(st.ex[j], 16u * cg + 15u, 1);
+        const uint32_t lane_off = __builtin_amdgcn_ubfe(st.ex[j], 16u * cg, 15);
         const uint32_t mc = c ? m : (m & ~1u);
         const uint32_t sst = mc & ~(mc << 1);
         const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
@@ -1765,8 +1764,8 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
         return;
     }
     const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
-    const uint32_t c = __builtin_amdgcn_ubfe(st.lw[j], cg, 1);
-    const uint32_t lane_off = cg ? (st.ex[j] >> 16) : (st.ex[j] & 0xFFFFu);
+    const uint32_t c = __builtin_amdgcn_ubfe(st.ex[j], 16u * cg + 15u, 1);
+    const uint32_t lane_off = __builtin_amdgcn_ubfe(st.ex[j], 16u * cg, 15);
     const uint32_t mc = c ? m : (m & ~1u);
     const uint32_t sst = mc & ~(mc << 1);
     const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
