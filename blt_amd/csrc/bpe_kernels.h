@@ -8,10 +8,7 @@ namespace blt {
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
 constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
-#ifndef BLT_TOKS
-#define BLT_TOKS 2                             // sub-tiles (of 16 wave ranges) per u16 scan tile
-#endif
-constexpr uint64_t kTilePosTok = 16384 * BLT_TOKS;   // tokens per look-back tile of the u16 scan kernel
+constexpr uint64_t kTilePosTok = 32768;        // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
 constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chunk-map word each)
 constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range

@@ -1560,7 +1560,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
 // A wave range whose output is its input (no merge before it in the buffer and none in it)
 // writes nothing, so a pass that merges nothing (the fixpoint check) only reads.
 // ===========================================================================================
-constexpr int kSt = BLT_TOKS;                              // sub-tiles per token tile
+constexpr int kSt = (int)(kTilePosTok / kTokRange) / kWaves;   // sub-tiles per token tile (2 at 16 waves)
 constexpr uint32_t kSubTok = (uint32_t)kWaves * kWavePos;   // tokens per sub-tile (16 wave ranges)
 constexpr uint32_t kTileTok = (uint32_t)kSt * kSubTok;
 constexpr int kGroupsTok = kSt * kWaves;

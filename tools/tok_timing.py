@@ -19,7 +19,7 @@ import torch  # noqa: E402
 import blt_amd  # noqa: E402
 from blt_amd import synth  # noqa: E402
 
-TOK_TILE = 16384 * int(os.environ.get("BLT_TOKS", "2"))
+TOK_TILE = 32768
 CHUNK = 16 << 20
 MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
 
