@@ -4,6 +4,7 @@
   audio (0xFF02, lib.rs:93-104): the stitched stream bit-exact against the C oracle, and the
   per-chunk token counts checked against the size-independent bounds (n/2 <= M <= n per chunk,
   offsets monotone, last offset = total).
+- f2: 3 GiB of text through a chained general map (u16 passes past 2^31 token bytes).
 - cfg4: 8 GiB of text cut into the 8 contiguous chunk ranges of an 8-GPU run (blt_amd.shard,
   the partition bench.py and blt_bpe_process_chunks use); every shard runs as its own launch
   and the rank-order stitch equals the one-shot oracle stream: sharding is exact.
@@ -71,3 +72,17 @@ def test_cfg4_eight_shards_8gib():
     del parts
     exp = O.COracle(m).run(text, CHUNK, threads=16)
     assert np.array_equal(got, exp)
+
+
+def test_general_map_3gib():
+    """f2 at scale: 3 GiB of text through the chained, byte-valued map (one byte pass, then u16
+    passes in place over ~2.9 G tokens, past 2^31 token bytes), 16 MiB chunks: stream and chunk
+    offsets bit-exact against the oracle, and the chain stops after one u16 pass."""
+    n = 3 << 30
+    text = synth.text(n, seed=7)
+    m = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
+    got, off = _device_encode(blt_amd.BpeStrategy(m), text, CHUNK)
+    assert blt_amd._lib.lib().blt_debug_last_u16_passes() == 1
+    exp, elens = O.COracle(m).run(text, CHUNK, threads=16, return_lens=True)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(np.diff(off) * 2, elens)
