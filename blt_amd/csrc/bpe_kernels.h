@@ -10,7 +10,10 @@ constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (k
 constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
 constexpr uint64_t kTilePosTok = 32768;        // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
 constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chunk-map word each)
-constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
+#ifndef BLT_TILE_BYTES
+#define BLT_TILE_BYTES 32768
+#endif
+constexpr uint64_t kTilePosBytes = BLT_TILE_BYTES;   // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 
