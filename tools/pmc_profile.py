@@ -1,6 +1,9 @@
 """Collects rocprofv3 PMC counters for the merge-scan kernel, one counter group per pass.
 
-    python tools/pmc_profile.py OUTDIR [--groups A,B,...] [--kernel NAME] [-- bench args]
+    python tools/pmc_profile.py OUTDIR [--groups A,B,...] [--kernel NAME] [--script S] [-- args]
+
+(--script: the profiled program instead of bench.py, e.g. tools/config_rates.py with
+`-- --only multi` for the u16 scan kernel of the general map.)
 
 Each group runs `rocprofv3 --pmc <counters> --kernel-trace --output-format csv -- python
 bench.py ...` as a child process (counters in their own passes, never with sys/runtime
@@ -33,11 +36,11 @@ GROUPS = {
 }
 
 
-def run_group(outdir, name, counters, bench_args, kernel):
+def run_group(outdir, name, counters, bench_args, kernel, script="bench.py"):
     d = os.path.join(outdir, name)
     os.makedirs(d, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
-           "--", sys.executable, os.path.join(ROOT, "bench.py"), *bench_args]
+           "--", sys.executable, os.path.join(ROOT, script), *bench_args]
     print("+", " ".join(cmd), flush=True)
     with open(os.path.join(d, "log.txt"), "w") as log:
         rc = subprocess.run(cmd, stdout=log, stderr=subprocess.STDOUT, timeout=900).returncode
@@ -63,6 +66,7 @@ def main():
     ap.add_argument("outdir")
     ap.add_argument("--groups", default=",".join(GROUPS))
     ap.add_argument("--kernel", default="scan_bytes_kernel")
+    ap.add_argument("--script", default="bench.py")
     argv = sys.argv[1:]
     extra = []
     if "--" in argv:
@@ -73,7 +77,7 @@ def main():
     os.makedirs(a.outdir, exist_ok=True)
     result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}}
     for g in a.groups.split(","):
-        vals, nd = run_group(a.outdir, g, GROUPS[g], bench_args, a.kernel)
+        vals, nd = run_group(a.outdir, g, GROUPS[g], bench_args, a.kernel, a.script)
         result["per_dispatch"].update(vals)
         result["dispatches"].update(nd)
     pd = result["per_dispatch"]
