@@ -507,6 +507,7 @@ WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     L.status = blt::kCtlBytes;
     L.zero_bytes = up16(blt::kCtlBytes + 8 * L.ntiles);
     L.total = L.zero_bytes;   // u64 [2] pass totals (alternating), u32 done flag, pad: 32 bytes
+                              // (right after pass 1's status words: encode_device zeroes both at once)
     L.off_a = L.total + 32;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
@@ -647,8 +648,11 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
                         reinterpret_cast<uint64_t*>(ws + L.off_b)};
     uint64_t* tot = reinterpret_cast<uint64_t*>(ws + L.total);
     uint32_t* done = reinterpret_cast<uint32_t*>(ws + L.total + 16);
-    HIP_TRY(hipMemsetAsync(tot, 0, 32, s));
-    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0])) return rc;
+    // pass 1's control block and status words and the chain's totals are contiguous: one memset
+    // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
+    HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + 32, s));
+    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0], true))
+        return rc;
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
