@@ -608,3 +608,39 @@ def test_token_scan_lds_two_choice_table():
     exp, elens = O.COracle(m).run(data, 1 << 20, threads=8, return_lens=True)
     assert np.array_equal(got, exp)
     assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_token_scan_random_general_maps(seed):
+    """Random general maps on the u16 scan kernel: chains of random depth whose values may be
+    bytes, new ids or ids near the u16 top, over skewed random bytes of a small alphabet (merge
+    densities from sparse to nearly every pair), odd chunk sizes, output and per-chunk lengths
+    against the oracle."""
+    rng = random.Random(1000 + seed)
+    alph = rng.choice([2, 3, 5, 8, 20])
+    letters = [97 + i for i in range(alph)]
+    toks = list(letters)
+    m = {}
+    nxt = rng.choice([256, 300, 65500])
+    for _ in range(rng.randrange(2, 60)):
+        a, b = rng.choice(toks), rng.choice(toks)
+        if (a, b) in m:
+            continue
+        r = rng.random()
+        if r < 0.15:
+            v = rng.choice(letters)              # byte-valued (tokenizer.rs:283-291)
+        else:
+            v = nxt & 0xFFFF
+            nxt += 1
+        m[(a, b)] = v
+        if v not in toks and rng.random() < 0.7:
+            toks.append(v)                       # a later key may chain on it (tokenizer.rs:204-212)
+    w = np.array([rng.random() ** 2 + 0.01 for _ in letters])
+    n = rng.choice([(1 << 19) + 3, (3 << 20) + 17, 2 << 20])
+    data = np.random.default_rng(seed).choice(np.array(letters, np.uint8), n, p=w / w.sum())
+    cs = rng.choice([4096, 4097, 12289, 65536, (1 << 20) + 1])
+    s = blt_amd.BpeStrategy(m)
+    got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp), (seed, m)
+    assert np.array_equal(lens, elens)
