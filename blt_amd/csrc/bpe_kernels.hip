@@ -277,6 +277,21 @@ template <> struct Seg<uint16_t> {
     static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
 };
 
+// Global -> LDS copy of n 16-byte units by nthr threads, kBatch loads in flight per thread
+// before their stores (a rolled loop waits for every load: one L2/MALL round trip each).
+template <int kBatch, typename T>
+__device__ __forceinline__ void copy_to_lds(T* dst, const T* src, uint32_t n, uint32_t tid, uint32_t nthr) {
+    for (uint32_t i0 = tid; i0 < n; i0 += kBatch * nthr) {
+        T v[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)   // unconditional (a clamped duplicate): no branch to wait at
+            v[k] = src[i0 + k * nthr < n ? i0 + k * nthr : n - 1];
+#pragma unroll
+        for (int k = 0; k < kBatch; ++k)
+            if (i0 + k * nthr < n) dst[i0 + k * nthr] = v[k];
+    }
+}
+
 // General-map lookup of the pair key BE(a) | BE(b) << 16 (the two u16 words as stored): both
 // candidate buckets are read (no probe loop); returns the matching bucket's value word,
 // BE(v) | 1 << 31, or 0.  The bucket is the top bits of v_dot2_u32_u16(key, hmul).
@@ -332,9 +347,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     if constexpr (kDense) {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
-        for (int i = tid; i < 65536 * 2 / 16; i += kThreads) dst[i] = src[i];
+        copy_to_lds<8>(dst, src, 65536u * 2u / 16u, (uint32_t)tid, (uint32_t)kThreads);
     } else if constexpr (kHashLds) {
-        for (uint32_t i = tid; i < p.hbytes / 8u; i += kThreads) s_hash[i] = p.hbuckets[i];
+        copy_to_lds<8>(s_hash, p.hbuckets, p.hbytes / 8u, (uint32_t)tid, (uint32_t)kThreads);
     }
 
     for (;;) {
@@ -1405,6 +1420,11 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t ntiles = p.ntiles;
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
 
+    // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
+    uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
+    if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
+    // the tickets first: a claim waits for its atomic, and the next one is claimed a round trip
+    // later (other workgroups' claims in between: measured, two consecutive tiles are slower)
     if (tid == 0) {
         s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);   // T
         s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);   // Tq, the tile after it
@@ -1414,9 +1434,22 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
-        for (int i = tid; i < (int)(kSelfEntries * 2 / 16); i += kThreads) dst[i] = src[i];
+        // LDS-DMA, every load in flight at once (one wave-instruction fills 1 KiB of LDS).  (A
+        // rolled copy loop waits for each load: one L2/MALL round trip each, ~0.7 us when all 256
+        // workgroups copy at once, 6.9 us in all.)
+        constexpr int kUnits = (int)(kSelfEntries * 2 / 16);
+        constexpr int kPer = (kUnits + kThreads - 1) / kThreads;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int u0 = (int)wave * 64 + k * kThreads;   // the wave's first unit (uniform)
+            if (k < kPer - 1 || u0 < kUnits)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void*)(src + u0 + lane),
+                    (__attribute__((address_space(3))) void*)(dst + u0), 16, 0, 0);
+        }
     }
     __syncthreads();
+    if (wg_rec && tid == 0) wg_rec[1] = __builtin_amdgcn_s_memrealtime();
     const uint32_t tab = uni(lds_addr(s_tab));
     uint32_t T = uni(s_tk[kRing - 2]);    // tile in phase 1
     uint32_t Tp = kNone;                  // tile waiting for emission
@@ -1569,6 +1602,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         if (!(T < ntiles || Tp < ntiles)) break;
         step(xb, nb, xa, na, sb, sa);
     }
+    if (wg_rec && lane == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(wg_rec + 2), (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ===========================================================================================
@@ -1853,16 +1888,26 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
         return (uint32_t)(l > 0x7FFFFFFFull ? 0x7FFFFFFFull : l);
     };
 
+    if constexpr (kHashLds) {
+        // LDS-DMA, all loads in flight (the LDS region is rounded up to whole KiB: a wave-
+        // instruction fills 1 KiB; the lanes past the table load its last unit again)
+        const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
+        uint4* dst = reinterpret_cast<uint4*>(s_tokhash);
+        const uint32_t nu = p.hbytes / 16u;
+#pragma unroll
+        for (uint32_t k = 0; k < kHashLdsMax / 16u / kThreads; ++k) {
+            const uint32_t u0 = wave * 64u + k * kThreads;   // uniform
+            if (u0 < nu)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) void*)(src + (u0 + lane < nu ? u0 + lane : nu - 1)),
+                    (__attribute__((address_space(3))) void*)(dst + u0), 16, 0, 0);
+        }
+    }
     if (tid == 0) {
         s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);
         s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
-    }
-    if constexpr (kHashLds) {
-        const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
-        uint4* dst = reinterpret_cast<uint4*>(s_tokhash);
-        for (uint32_t i = tid; i < p.hbytes / 16u; i += kThreads) dst[i] = src[i];
     }
     __syncthreads();
     const uint32_t tab = kHashLds ? uni(lds_addr(s_tokhash)) : 0u;
@@ -2156,7 +2201,7 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
                      : mode == 1 ? (const void*)seg::scan_tokens_kernel<1> : (const void*)seg::scan_tokens_kernel<0>;
     const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
     const int grid = grid_for(ntiles, device, fn, seg::kThreads, 5 + mode);
-    const size_t smem = lds ? p.hbytes : 0;
+    const size_t smem = lds ? ((size_t)p.hbytes + 1023) & ~(size_t)1023 : 0;   // whole KiB (LDS-DMA rows)
     const dim3 g((unsigned)grid), b(seg::kThreads);
     if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2>), g, b, smem, s, p);
     else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1>), g, b, smem, s, p);

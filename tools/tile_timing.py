@@ -35,7 +35,7 @@ def main():
     wsb = s.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     ntiles = (n + TILE - 1) // TILE
-    dbg = torch.zeros((8 + 8 * 16) * ntiles, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros((8 + 8 * 16) * ntiles + 4 * 4096, dtype=torch.int64, device="cuda")
     L = blt_amd._lib.lib()
     L.blt_debug_set_tile_record.argtypes = [ctypes.c_void_p]
     sp = torch.cuda.current_stream().cuda_stream
@@ -44,8 +44,20 @@ def main():
         s.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
     L.blt_debug_set_tile_record(None)
     rec = dbg.cpu().numpy().astype(np.int64)
+    # workgroup start / table copied / exit (s_memrealtime, 100 MHz) against the tiles' publishes
+    wg = rec[(8 + 8 * 16) * ntiles:].reshape(-1, 4)
+    wg = wg[wg[:, 0] > 0]
+    if wg.size:
+        t0 = wg[:, 0].min()
+        us_ = lambda v: (v - t0) / 100.0
+        pubs = rec[4 * ntiles:8 * ntiles:4]
+        pubs = pubs[pubs > 0]
+        print(f"{len(wg)} workgroups: start us p50 {np.median(us_(wg[:, 0])):.2f} max {us_(wg[:, 0]).max():.2f}; "
+              f"table copied p50 {np.median(us_(wg[:, 1])):.2f} max {us_(wg[:, 1]).max():.2f}; "
+              f"exit p50 {np.median(us_(wg[:, 2])):.2f} max {us_(wg[:, 2]).max():.2f}; "
+              f"tile publishes first {us_(pubs.min()):.2f} last {us_(pubs.max()):.2f}")
     how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
-    wv8 = rec[8 * ntiles:].reshape(ntiles, 16, 8)
+    wv8 = rec[8 * ntiles:(8 + 8 * 16) * ntiles].reshape(ntiles, 16, 8)
     wv = wv8[:, :, :6]
     ok = wv[:, 0, :].sum(axis=1) > 0
     wv = wv[ok]
