@@ -1,7 +1,8 @@
 """Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook, in
 the timing build build/exp/libblt_bpe_timing.so from `make exp`, or BLT_LIB_PATH).
 
-    python tools/tile_timing.py [MiB] [--random]     (--random: cfg5's random bytes instead of cfg3's text)
+    python tools/tile_timing.py [MiB] [--random] [--few]   (--random: cfg5's random bytes instead of cfg3's
+    text; --few: a two-merge map, ~1 token per byte)
 Prints mean/median cycles of phase 1 (lookups + wave functions), phase 2 (tile resolve +
 look-back), phase 3 (emission + copy-out) and the look-back window statistics."""
 import ctypes
@@ -27,7 +28,10 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     mib = int(args[0]) if args else 1024
     n = mib << 20
-    merges = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
+    if "--few" in sys.argv:   # two merges ("e ", "th"): ~0.97 tokens per byte, two-part emission
+        merges = {(101, 32): 256, (116, 104): 257}
+    else:
+        merges = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
     s = blt_amd.BpeStrategy(merges)
     data = synth.random_bytes(n, seed=5) if "--random" in sys.argv else synth.text(n, seed=3)   # cfg5 / cfg3
     d_in = torch.from_numpy(data).cuda()
