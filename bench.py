@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("BLT_CPU_THREADS", "0")),
                     help="0: every usable host core (num_cpus semantics)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py output)")
+                    help="PMC-derived HBM bytes per launch (from tools/pmc_profile.py runs)")
     return ap.parse_args()
 
 
