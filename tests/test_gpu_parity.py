@@ -644,3 +644,24 @@ def test_token_scan_random_general_maps(seed):
     exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
     assert np.array_equal(got, exp), (seed, m)
     assert np.array_equal(lens, elens)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_byte_maps_chunked(seed):
+    """Random byte-pair maps (single-pass: ids from 256 up, none a key component) over skewed
+    random bytes, random lengths and chunk sizes from 1 byte to 1 MiB (the byte scan kernel at
+    >= 4096, the generic kernel below), output and per-chunk lengths against the oracle."""
+    rng = random.Random(2000 + seed)
+    alph = rng.choice([2, 4, 16, 64, 256])
+    density = rng.choice([0.02, 0.2, 0.6] + ([1.0] if alph < 256 else []))
+    nkeys = int(density * alph * alph)
+    m = _rand_bytepair_map(rng, density, alphabet=alph, base=rng.choice([256, 1000, 65536 - nkeys]))
+    w = np.array([rng.random() ** 3 + 0.001 for _ in range(alph)])
+    n = rng.choice([1, 4095, 4097, 100_000, (1 << 20) + 5, 3 << 20])
+    data = np.random.default_rng(seed).choice(np.arange(alph, dtype=np.uint8), n, p=w / w.sum())
+    cs = rng.choice([1, 7, 1000, 4096, 4099, 65536, 1 << 20])
+    s = blt_amd.BpeStrategy(m)
+    got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    assert np.array_equal(got, exp), (seed, alph, density, n, cs)
+    assert np.array_equal(lens, elens)
