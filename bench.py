@@ -71,25 +71,27 @@ def usable_cores():
     return int(_lib.lib().blt_determine_thread_count(0, 0)), aff, os.cpu_count() or 1
 
 
-def kernel_ms(strategy, d_in, n, d_out, reps=20):
-    """Median kernel time (HIP events on the launch stream, workspace reset outside them)."""
+def kernel_ms(strategy, d_in, n, d_out, reps=20, warmup=5):
+    """Median kernel time (HIP events on the launch stream, workspace reset outside them), after
+    `warmup` untimed launches, the launches back to back: as the timed loop of `value`."""
     import torch
     wsb = strategy.workspace_size(n, CHUNK)
     ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     tok = strategy.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
-    ts = []
-    for _ in range(reps):
+    for _ in range(warmup):
         strategy.workspace_reset(ws.data_ptr(), n, CHUNK, sp)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        strategy.encode_device_prezeroed(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        strategy.workspace_reset(ws.data_ptr(), n, CHUNK, sp)
         e0.record(stream)
         strategy.encode_device_prezeroed(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp)
         e1.record(stream)
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
+    torch.cuda.synchronize()
     strategy.check_workspace(ws.data_ptr(), sp)
-    return float(np.median(ts)), tok
+    return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), tok
 
 
 def workload(synth, name, n):
