@@ -14,7 +14,7 @@ ORACLE := oracle/liboracle.so
 CLI := blt_amd/blt
 OBJDIR := build
 
-all: $(LIB) $(SYNTH) $(ORACLE) $(CLI) sanitize
+all: $(LIB) $(SYNTH) $(ORACLE) $(CLI)
 
 $(OBJDIR):
 	mkdir -p $(OBJDIR)

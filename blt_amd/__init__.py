@@ -212,6 +212,14 @@ class BpeStrategy(TokenizationStrategy):
         _lib.check(self._L.blt_bpe_encode_device_ex(self._h, d_in, n, chunk_size, d_out, d_chunk_off or None,
                                                     d_workspace, workspace_bytes, stream or None, None, 1))
 
+    def clear_error(self) -> bool:
+        """blt_bpe_clear_error: resets the handle's sticky device error (every call fails with
+        BltError(BLT_E_IO) after a kernel of the handle flagged one).  True if one was pending."""
+        rc = self._L.blt_bpe_clear_error(self._h)
+        if rc not in (0, _lib.BLT_E_IO):
+            _lib.check(rc)
+        return rc == _lib.BLT_E_IO
+
     def check_workspace(self, d_workspace: int, stream: int = 0) -> None:
         _lib.check(self._L.blt_bpe_check_workspace(d_workspace, stream or None))
 
@@ -309,13 +317,18 @@ class ByteTokenizer:
     e.g. "16MB" (utils.rs:10-45); ``memory_cap``: percent of RAM for the automatic chunk size
     (0-100, lib.rs:57-63).
 
-    Documented deviation: the reference writes the dict's KEYS to a temporary merges file in
-    HashMap iteration order (lib.rs:106-113), so its token ids are 256 + that (random) order and the
-    dict's values are ignored; here the ids are the dict's values, deterministically.
+    Token ids follow the reference binding: it writes the dict's KEYS, one "a b" line each, to a
+    temporary merges file and loads that file (lib.rs:103-114, config_loader.rs:14-46), so the ids
+    are 256, 257, ... in the order the keys are written and the dict's values are ignored.  The
+    reference writes them in HashMap iteration order (random per process); here they are written in
+    the dict's insertion order, which is one of the reference's possible outcomes, and the same
+    temporary-file load runs (so every loader rule applies, the u16 wrap past 65,280 keys included).
+    ``use_dict_ids=True`` (not in the reference) takes the dict's values as the ids instead.
     """
 
     def __init__(self, merges: Optional[Dict[Tuple[int, int], int]] = None, content_type: Optional[str] = None,
-                 threads: Optional[int] = None, chunk_size: Optional[str] = None, memory_cap: Optional[int] = None):
+                 threads: Optional[int] = None, chunk_size: Optional[str] = None, memory_cap: Optional[int] = None,
+                 *, use_dict_ids: bool = False):
         if merges is not None:
             if not isinstance(merges, dict):
                 raise TypeError("merges must be a dict {(byte1, byte2): token_id}")
@@ -338,6 +351,7 @@ class ByteTokenizer:
         self._threads = threads
         self._chunk_size = chunk_size
         self._memory_cap = memory_cap
+        self._use_dict_ids = bool(use_dict_ids)
 
     def tokenize_file(self, input_path: str, output_path: str) -> None:
         """lib.rs:90-159: CoreConfig::new_from_cli + run_tokenizer on the two files.  Raises OSError
@@ -353,13 +367,28 @@ class ByteTokenizer:
             cli_cs = out.value
         mem_cap = 80 if self._memory_cap is None else self._memory_cap   # lib.rs:172
         cs = get_effective_chunk_size(cli_cs, threads, mem_cap)
-        strategy = BpeStrategy(self._merges) if self._merges is not None else BasicTokenizationStrategy()
+        strategy = self._strategy()
         token = {"Text": ContentType.Text, "Bin": ContentType.Bin}.get(self._content_type)
         try:
             file_tokenizer(os.fspath(input_path), os.fspath(output_path), strategy, token, threads, cs)
         finally:
             if isinstance(strategy, BpeStrategy):
                 strategy.close()
+
+    def _strategy(self) -> TokenizationStrategy:
+        if self._merges is None:
+            return BasicTokenizationStrategy()
+        if self._use_dict_ids:
+            return BpeStrategy(self._merges)
+        import tempfile
+        # lib.rs:103-114: the keys, one "a b" line each, then the file goes through the loader
+        fd, path = tempfile.mkstemp(prefix="blt_merges_", suffix=".txt")
+        try:
+            with os.fdopen(fd, "w") as f:
+                f.write("".join(f"{a} {b}\n" for a, b in self._merges))
+            return BpeStrategy.from_file(path)
+        finally:
+            os.unlink(path)
 
     def __repr__(self) -> str:   # lib.rs:162-170
         return (f"ByteTokenizer(merges={len(self._merges) if self._merges is not None else 0}, "

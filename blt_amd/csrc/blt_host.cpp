@@ -265,8 +265,10 @@ struct blt_bpe {
     // an error (look-back timeout, output range, prefix invariant) stores 1 here, and every later
     // call on the handle fails with BLT_E_IO until blt_bpe_clear_error.  An async encode cannot
     // report its own failure, but the caller's next call does.
+    // Published once under sticky_once with a release store; read with acquire loads, so a thread
+    // that checks it before its own first sticky_word() never races the allocating thread.
     std::once_flag sticky_once;
-    uint32_t* sticky = nullptr;
+    std::atomic<uint32_t*> sticky{nullptr};
 };
 
 namespace {
@@ -463,15 +465,15 @@ uint32_t* sticky_word(const blt_bpe* hc) {
         void* p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) == hipSuccess) {
             memset(p, 0, 64);
-            h->sticky = static_cast<uint32_t*>(p);
+            h->sticky.store(static_cast<uint32_t*>(p), std::memory_order_release);
         }
     });
-    return h->sticky;
+    return h->sticky.load(std::memory_order_acquire);
 }
 
 // BLT_E_IO if a kernel of this handle flagged a device error since the last blt_bpe_clear_error.
 int sticky_check(const blt_bpe* h) {
-    const uint32_t* w = h->sticky;
+    const uint32_t* w = h->sticky.load(std::memory_order_acquire);
     if (w && __atomic_load_n(w, __ATOMIC_ACQUIRE))
         return fail(BLT_E_IO,
                     "a previous merge scan on this handle flagged a device error (look-back timeout, output range "
@@ -592,7 +594,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
         p.cs_tiles_magic = p.cs_tiles > 1 ? (uint32_t)(0xFFFFFFFFull / p.cs_tiles) : 0u;
     }
     p.debug = g_debug_tiles;
-    p.sticky = h->sticky;
+    p.sticky = h->sticky.load(std::memory_order_acquire);
     p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));
     else if (in_u16 && tok_scan) HIP_TRY(blt::launch_scan_tokens(p, dev, s));
@@ -667,7 +669,17 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         }
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (int rc = sticky_check(h)) return rc;
+        if (sticky_check(h)) {
+            // the control block holds the flags and first-error record of the chain's u16 scan
+            // passes (their chunk-map kernel resets only the ticket); report them with the sticky
+            // message
+            const std::string sticky_msg = t_err;
+            uint32_t ctl[16] = {0};
+            if (hipMemcpy(ctl, ws + L.ctl, sizeof ctl, hipMemcpyDeviceToHost) == hipSuccess && ctl_error(ctl))
+                return fail(BLT_E_IO, "%s; u16 passes 1..%llu: %s", sticky_msg.c_str(), (unsigned long long)(k - 1),
+                            t_err.c_str());
+            return fail(BLT_E_IO, "%s", sticky_msg.c_str());
+        }
         if ((uint32_t)rec[2]) break;
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
@@ -926,7 +938,7 @@ namespace {
 
 // cgroup CPU quota as num_cpus 1.17 reads it (cgroup v2 cpu.max, v1 cfs quota/period): ceil(quota /
 // period), 0 when unlimited or unreadable.
-uint64_t cgroup_cpus() {
+uint64_t cgroup_cpus(const char* root, const char* proc_cgroup) {
     auto read_two = [](const std::string& path, std::string& a, std::string& b) {
         FILE* f = fopen(path.c_str(), "r");
         if (!f) return false;
@@ -947,7 +959,7 @@ uint64_t cgroup_cpus() {
     };
     // the process's own cgroup (v2: "0::/path")
     std::string rel;
-    if (FILE* f = fopen("/proc/self/cgroup", "r")) {
+    if (FILE* f = fopen(proc_cgroup, "r")) {
         char line[512];
         while (fgets(line, sizeof line, f))
             if (strncmp(line, "0::", 3) == 0) {
@@ -957,19 +969,18 @@ uint64_t cgroup_cpus() {
         fclose(f);
     }
     std::string a, b;
-    for (const std::string& base : {std::string("/sys/fs/cgroup") + (rel == "/" ? "" : rel), std::string("/sys/fs/cgroup")})
+    const std::string r(root);
+    for (const std::string& base : {r + (rel == "/" ? "" : rel), r})
         if (read_two(base + "/cpu.max", a, b)) return a == "max" ? 0 : ceil_div(a, b);
     std::string q, per, unused;
-    if (read_two("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", q, unused) &&
-        read_two("/sys/fs/cgroup/cpu/cpu.cfs_period_us", per, unused))
+    if (read_two(r + "/cpu/cpu.cfs_quota_us", q, unused) && read_two(r + "/cpu/cpu.cfs_period_us", per, unused))
         return ceil_div(q, per);
     return 0;
 }
 
-// num_cpus::get() (utils.rs:79-97 uses it): the cgroup quota when there is one, otherwise the CPUs
-// this process may run on (sched_getaffinity), otherwise the online CPUs.
-uint64_t available_cpus() {
-    if (const uint64_t q = cgroup_cpus()) return q;
+// num_cpus 1.17's logical_cpus(): the CPUs this process may run on (sched_getaffinity), else the
+// online CPUs.
+uint64_t logical_cpus() {
     cpu_set_t set;
     CPU_ZERO(&set);
     if (sched_getaffinity(0, sizeof set, &set) == 0) {
@@ -978,6 +989,15 @@ uint64_t available_cpus() {
     }
     const long c = sysconf(_SC_NPROCESSORS_ONLN);
     return c > 0 ? (uint64_t)c : 1;
+}
+
+// num_cpus::get() (utils.rs:79-97 uses it): with a cgroup CPU quota, min(quota, logical_cpus())
+// (num_cpus 1.17 init_cgroups; crate not vendored in the reference, restated), else logical_cpus().
+uint64_t available_cpus(const char* cgroup_root = "/sys/fs/cgroup", const char* proc_cgroup = "/proc/self/cgroup",
+                        uint64_t logical = 0) {
+    if (!logical) logical = logical_cpus();
+    if (const uint64_t q = cgroup_cpus(cgroup_root, proc_cgroup)) return std::min(q, logical);
+    return logical;
 }
 
 }  // namespace
@@ -1109,7 +1129,7 @@ void blt_bpe_destroy(blt_bpe* h) {
         if (h->dev[d].self_be) (void)hipFree(h->dev[d].self_be);
         if (h->dev[d].hbuckets) (void)hipFree(h->dev[d].hbuckets);
     }
-    if (h->sticky) (void)hipHostFree(h->sticky);
+    if (uint32_t* w = h->sticky.load(std::memory_order_acquire)) (void)hipHostFree(w);
     delete h;
 }
 
@@ -1122,7 +1142,7 @@ int blt_bpe_info(const blt_bpe* h, size_t* n_entries, int* single_pass) {
 
 int blt_bpe_clear_error(const blt_bpe* h) {
     if (!h) return fail(BLT_E_INVALID_INPUT, "null handle");
-    uint32_t* w = h->sticky;
+    uint32_t* w = h->sticky.load(std::memory_order_acquire);
     if (!w || !__atomic_exchange_n(w, 0u, __ATOMIC_ACQ_REL)) return 0;
     return fail(BLT_E_IO, "a merge scan on this handle had flagged a device error (now cleared)");
 }
@@ -1164,6 +1184,12 @@ int blt_bpe_check_workspace(void* d_ws, void* stream) {
         return fail(rc, "%s", msg.c_str());
     }
     return 0;
+}
+
+// Not in the public header: num_cpus::get() over a given cgroup root, /proc/self/cgroup file and
+// logical CPU count (tests: fake cgroup trees).
+uint64_t blt_debug_available_cpus(const char* cgroup_root, const char* proc_cgroup, uint64_t logical) {
+    return available_cpus(cgroup_root, proc_cgroup, logical);
 }
 
 // Not in the public header: a test hook that makes every merge pass record, per tile, its

@@ -1654,14 +1654,15 @@ __device__ __forceinline__ bool pass_done(const PassParams& p) {
 }
 
 // One thread per wave range: lower bound of the range start in the chunk starts.  It also zeroes
-// the scan's control block and status words (one per kTileTok tokens, so the wave ranges cover
-// them): the previous pass has finished with them.
+// the scan's ticket and status words (one per kTileTok tokens, so the wave ranges cover them): the
+// previous pass has finished with them.  The error flags and first-error record (ctl[1..]) stay,
+// so the host reports the chain's first failure (the chain's first memset zeroed them).
 __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     if (pass_done(p)) return;
     const uint64_t n = token_count(p);
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
-    if (r < kCtlBytes / 4) p.ctl[r] = 0u;
+    if (r == 0) p.ctl[0] = 0u;
     const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
     if (lo >= n) return;
     const uint64_t* cs = p.cstart;

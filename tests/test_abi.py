@@ -139,6 +139,35 @@ def test_thread_count(kats):
     assert blt_amd.determine_thread_count(None) >= 1
 
 
+def _cpus(root, proc, logical):
+    return _lib.lib().blt_debug_available_cpus(str(root).encode(), str(proc).encode(), logical)
+
+
+def test_available_cpus_fake_cgroups(tmp_path):
+    """num_cpus::get() (utils.rs:79-97 calls it): min(cgroup quota, logical CPUs) with a quota
+    (num_cpus 1.17 init_cgroups, restated: the crate is not vendored), else the logical CPUs."""
+    proc = tmp_path / "proc_cgroup"
+    proc.write_text("0::/job\n")
+    v2 = tmp_path / "v2"
+    (v2 / "job").mkdir(parents=True)
+    (v2 / "job" / "cpu.max").write_text("1600000 100000\n")   # quota 16 CPUs
+    assert _cpus(v2, proc, 256) == 16                           # quota below the affinity mask
+    assert _cpus(v2, proc, 8) == 8                              # quota above it: capped
+    (v2 / "job" / "cpu.max").write_text("150000 100000\n")     # 1.5 CPUs: ceil
+    assert _cpus(v2, proc, 64) == 2
+    (v2 / "job" / "cpu.max").write_text("max 100000\n")        # no quota
+    assert _cpus(v2, proc, 64) == 64
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("400000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert _cpus(v1, tmp_path / "missing", 12) == 4
+    assert _cpus(v1, tmp_path / "missing", 3) == 3
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert _cpus(v1, tmp_path / "missing", 12) == 12
+    assert _cpus(tmp_path / "none", tmp_path / "missing", 5) == 5
+
+
 def test_strategy_handle_info():
     s = blt_amd.BpeStrategy({(97, 98): 256, (99, 100): 257})
     assert s.info() == (2, True)

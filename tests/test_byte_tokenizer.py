@@ -152,33 +152,62 @@ def test_configuration_options_and_content_type(tmp_path):   # test_tokenizer.py
     assert dst.read_bytes() == b"\xff\x01" + _basic(b"test data for configuration")
 
 
+def test_dict_ids_follow_the_loader():
+    """lib.rs:103-114 writes the keys to a merges file and loads it: ids 256 + key order, values
+    ignored.  A dict whose values chain (120 feeds (120, 99)) is then single-pass; with
+    use_dict_ids its values are the ids and it is not.  No GPU: handle creation is host-only."""
+    merges = {(97, 98): 120, (120, 99): 300, (100, 100): 97}
+    s = blt.ByteTokenizer(merges=merges)._strategy()
+    assert s.info() == (3, True)
+    s.close()
+    s = blt.ByteTokenizer(merges=merges, use_dict_ids=True)._strategy()
+    assert s.info() == (3, False)
+    s.close()
+
+
+def test_dict_ids_wrap_like_the_loader():
+    """Every byte pair as a key: the loader's u16 counter wraps after 65,280 lines
+    (config_loader.rs:18, :40), so the last 256 keys get ids 0..255 and the map needs passes."""
+    merges = {(a, b): 1 for a in range(256) for b in range(256)}
+    s = blt.ByteTokenizer(merges=merges)._strategy()
+    assert s.info() == (65536, False)
+    s.close()
+
+
 @pytest.mark.gpu
 def test_large_data_bpe_bit_exact(tmp_path):
-    """A multi-chunk file with a 300-pair merge map whose ids are the dict's values (the
-    documented deviation), against the C oracle chunked at the same size."""
+    """A multi-chunk file with a 300-pair merge map: ids 256 + the dict's key order (the
+    reference binding's temporary merges file), then with use_dict_ids the dict's values; both
+    against the C oracle chunked at the same size."""
     from blt_amd import synth
     from oracle import oracle as O
     text = synth.text(3 * (1 << 20) + 12345, seed=21)
     pairs = synth.top_pair_merges(text, 300)
     rng = np.random.default_rng(4)
-    ids = rng.permutation(np.arange(256, 256 + 300))   # values, not line order
+    ids = rng.permutation(np.arange(256, 256 + 300))
     merges = {p: int(i) for p, i in zip(pairs, ids)}
     src, dst = tmp_path / "in", tmp_path / "out"
     src.write_bytes(text.tobytes())
     blt.ByteTokenizer(merges=merges, chunk_size="256KB", content_type="Bin").tokenize_file(str(src), str(dst))
+    line_ids = {p: 256 + i for i, p in enumerate(merges)}
+    exp = O.COracle(line_ids).run(text, 256 << 10, threads=4).tobytes()
+    assert dst.read_bytes() == b"\xff\x03" + exp
+    blt.ByteTokenizer(merges=merges, chunk_size="256KB", content_type="Bin",
+                      use_dict_ids=True).tokenize_file(str(src), str(dst))
     exp = O.COracle(merges).run(text, 256 << 10, threads=4).tobytes()
     assert dst.read_bytes() == b"\xff\x03" + exp
 
 
 @pytest.mark.gpu
 def test_chained_merges_from_dict(tmp_path):
-    """A dict whose values feed other keys needs several passes (tokenizer.rs:63-86)."""
+    """With use_dict_ids, a dict whose values feed other keys needs several passes
+    (tokenizer.rs:63-86)."""
     from oracle import oracle as O
     merges = {(97, 98): 120, (120, 99): 300, (100, 100): 97}
     data = (b"abcabcddbxabc" * 5000)
     src, dst = tmp_path / "in", tmp_path / "out"
     src.write_bytes(data)
-    blt.ByteTokenizer(merges=merges, chunk_size="256KB").tokenize_file(str(src), str(dst))
+    blt.ByteTokenizer(merges=merges, chunk_size="256KB", use_dict_ids=True).tokenize_file(str(src), str(dst))
     exp = O.COracle(merges).run(np.frombuffer(data, np.uint8), 256 << 10, threads=2).tobytes()
     assert dst.read_bytes() == exp
 

@@ -245,8 +245,8 @@ def test_sticky_device_error():
     with pytest.raises(blt_amd.BltError):
         s.check_workspace(ws.data_ptr(), sp)   # the workspace's flag (bit 1) ...
     s.check_workspace(ws.data_ptr(), sp)       # ... read and cleared
-    assert L.blt_bpe_clear_error(s.handle) == _lib.BLT_E_IO   # reports once, clears
-    assert L.blt_bpe_clear_error(s.handle) == 0
+    assert s.clear_error() is True    # reports once, clears
+    assert s.clear_error() is False
     assert s.encode_device(*args, sync=True) == tok
     assert np.array_equal(d_out[:2 * tok].cpu().numpy(), O.COracle(m).run(data, cs, threads=4))
 
