@@ -1,32 +1,40 @@
 """Benchmark of the BPE merge scan (BASELINE.json metric: input GB/s tokenized, % HBM roofline).
 
-Workload (per GPU): BASELINE config 3 — 1 GiB of seeded synthetic English-like text, the
-50 000-line merges built from that text (every pair seen, by frequency, then a seeded
-permutation of the rest), --chunksize 16MB.  One step = one whole-buffer merge pass over the
-rank's 1 GiB, inputs resident in HBM.  With N GPUs each rank tokenises its own 1 GiB shard of
-an N GiB stream (config 4's sharding; chunks are independent, so no collective on the data
-path) and `value` is the aggregate input rate: N x 1 GiB / max-over-ranks step time.
+Workloads (one step = one whole-buffer merge pass over each rank's shard, inputs
+resident in HBM; chunks are independent, so ranks share nothing and no collective touches the data):
+  cfg3 (default at N = 1): 1 GiB of seeded synthetic English-like text per GPU, the 50 000-line
+       merges built from that text, --chunksize 16MB (weak scaling: 1 GiB per rank at any N);
+  cfg4 (default at N > 1): ONE 8 GiB stream of the same text split over the N ranks by whole
+       chunks (shard.rank_bytes: 4 / 2 / 1 GiB per rank at N = 2 / 4 / 8; strong scaling);
+  cfg5: ONE 4 GiB stream of uniform random bytes, cfg3's merges, split the same way (strong);
+  cfg2: 100 MiB of text with 256 merges ranked from it (one GPU).
+--total-bytes overrides the stream size of cfg4 / cfg5.  `value` = bytes all ranks processed /
+max-over-ranks step time; `config.rank_bytes` lists every rank's byte range of the stream.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg4|cfg5|cfg2]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 Prints ONE JSON line on rank 0.  `roofline` prices the merge-scan kernel alone (HIP events on
 its stream around each launch) against HBM: algorithmic bytes = input bytes + 2 x output
-tokens.  `cpu_baseline` times the C restatement of the reference (hash-map, multi-pass,
-task-per-chunk) on the same 1 GiB with one thread per usable host core (num_cpus semantics: the
-cgroup quota, else the affinity mask; both counts are reported), and its output doubles as the
-bit-exact check of the GPU output; `cpu_baseline_optimized` times a dense-table single-pass CPU
-version beside it.
+tokens; `traffic` is the PMC-measured HBM bytes per launch from profiles/traffic.json, used only
+when that record names this workload, size and the sha256 of the kernel source it was measured
+on (else null).  `cpu_baseline` times the C restatement of the reference (hash-map, multi-pass,
+task-per-chunk) on rank 0's shard (N = 1 only) with one thread per usable host core (num_cpus
+semantics: min(cgroup quota, affinity mask)); its output doubles as the bit-exact check of the
+GPU output; `cpu_baseline_optimized` times a dense-table single-pass CPU version beside it.
 
-At N = 1 the line also carries (rank 0, outside the timed region of `value`):
-  * `configs`: the other BASELINE workloads on the same kernel, device-resident, kernel-only
-    (median of HIP-event timings), each with its roofline fraction and a bit-exact check:
-    cfg2 (100 MiB text, 256 merges) and cfg5 (1 GiB random bytes, cfg3's 50k merges); `multi`:
-    the f2 general map (256 MiB text, chained merges: one byte pass and u16 passes);
+At N = 1 with the cfg3 workload the line also carries (rank 0, outside the timed region):
+  * `configs`: the other workloads device-resident, kernel-only (median of HIP-event timings),
+    each with its roofline fraction and a bit-exact check: cfg2, cfg5 (the whole 4 GiB stream on
+    one GPU), and the general maps of row f2 (the whole encode_device call: byte pass, u16 passes,
+    the host's read of the pass count): `multi` (chained + byte-valued merges on text), `wrap`
+    (the 65 537-line merges file whose ids wrap: the L2 bucket table), `selfval` (merges valued
+    their own first byte: the generic byte pass), `chain` (a 24-level doubling chain: u16 passes
+    down to the generic token pass);
   * `end_to_end`: cfg3 through blt_bpe_process_chunks from pageable host memory (PCIe-inclusive);
-  * `per_chunk_path`: 16 host threads calling blt_bpe_process_chunk on the 64 16-MiB chunks of
-    cfg3 (the reference's per-chunk strategy calls, pipeline.rs:86, :141-150).
---workload cfg2|cfg5 makes that workload the timed one (for per-workload rocprofv3 runs).
+  * `per_chunk_path`: 16 host threads calling blt_bpe_process_chunk on the 64 16-MiB chunks;
+  * `cli_end_to_end`: the `blt` command line on cfg3's 1 GiB as a file on tmpfs to a tmpfs
+    output (the reference's only published figure is its binary's file rate, README.md:272-278).
 """
 import argparse
 import json
@@ -51,10 +59,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--bytes-per-gpu", type=int, default=GIB)
+    ap.add_argument("--bytes-per-gpu", type=int, default=GIB, help="cfg3's bytes per rank")
+    ap.add_argument("--total-bytes", type=int, default=0, help="cfg4 / cfg5 stream size (default 8 GiB / 4 GiB)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip configs / end_to_end / per_chunk_path")
-    ap.add_argument("--workload", default="cfg3", choices=["cfg2", "cfg3", "cfg5"])
+    ap.add_argument("--no-extra", action="store_true", help="skip configs / end_to_end / per_chunk_path / cli")
+    ap.add_argument("--only-configs", default="", help="comma list: run only these `configs` rows")
+    ap.add_argument("--workload", default="", choices=["", "cfg2", "cfg3", "cfg4", "cfg5"],
+                    help="default: cfg3 at N = 1, cfg4 at N > 1")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("BLT_CPU_THREADS", "0")),
                     help="0: every usable host core (num_cpus semantics)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -94,25 +105,42 @@ def kernel_ms(strategy, d_in, n, d_out, reps=20, warmup=5):
     return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), tok
 
 
-def workload(synth, name, n):
-    """(host bytes, merges, description) of a BASELINE workload."""
+STRONG_TOTAL = {"cfg4": 8 * GIB, "cfg5": 4 * GIB}
+
+
+def workload(synth, name, rank=0, world=1, per_gpu=GIB, total=0):
+    """(host bytes of this rank's shard, merges, description, (b0, b1) of the stream, stream bytes)
+    of a BASELINE workload."""
     if name == "cfg2":
         host = synth.text(100 << 20, seed=2)
         return host, synth.merges_dict(synth.top_pair_merges(host, 256)), \
-            "cfg2: 100 MiB synthetic text, 256 merges ranked from it, --chunksize 16MB"
+            "cfg2: 100 MiB synthetic text, 256 merges ranked from it, --chunksize 16MB", (0, host.size), host.size
     merges = build_merges(synth)
-    if name == "cfg5":
-        return synth.random_bytes(n, seed=5), merges, \
-            f"cfg5 (per-GPU share): {n >> 20} MiB random bytes, cfg3's 50000-line merges, --chunksize 16MB"
-    return None, merges, f"cfg3: {n >> 30} GiB synthetic text per GPU, 50000-line merges, --chunksize 16MB"
+    from blt_amd import shard
+    if name == "cfg3":   # weak: 1 GiB per rank, rank r's slice of an N GiB stream
+        stream = world * per_gpu
+        b0, b1 = shard.rank_bytes(stream, CHUNK, rank, world)
+        return synth.text(b1 - b0, seed=3, offset=b0), merges, \
+            f"cfg3: {per_gpu >> 20} MiB synthetic text per GPU, 50000-line merges, --chunksize 16MB", (b0, b1), stream
+    stream = total or STRONG_TOTAL[name]
+    b0, b1 = shard.rank_bytes(stream, CHUNK, rank, world)
+    if name == "cfg4":
+        return synth.text(b1 - b0, seed=3, offset=b0), merges, \
+            f"cfg4: one {stream >> 20} MiB synthetic-text stream split over {world} GPU(s), 50000-line merges, " \
+            f"--chunksize 16MB", (b0, b1), stream
+    return synth.random_bytes(b1 - b0, seed=5, offset=b0), merges, \
+        f"cfg5: one {stream >> 20} MiB random-byte stream split over {world} GPU(s), cfg3's 50000-line merges, " \
+        f"--chunksize 16MB, --type audio", (b0, b1), stream
 
 
-def extra_configs(blt_amd, synth, O, threads):
-    """cfg2 and cfg5 on the same kernel (kernel-only rates, bit-exact against the oracle)."""
+def extra_configs(blt_amd, synth, O, threads, only=()):
+    """cfg2, cfg5 and the f2 general maps (kernel-only rates, bit-exact against the oracle)."""
     import torch
     res = {}
     for name in ("cfg2", "cfg5"):
-        host, merges, desc = workload(synth, name, GIB)
+        if only and name not in only:
+            continue
+        host, merges, desc, _, _ = workload(synth, name)
         s = blt_amd.BpeStrategy(merges)
         n = host.size
         d_in = torch.from_numpy(host).cuda()
@@ -121,28 +149,59 @@ def extra_configs(blt_amd, synth, O, threads):
         got = d_out[:2 * tok].cpu().numpy()
         exp = O.COracle(merges).run(host, CHUNK, threads=threads)
         algo = n + 2 * tok
-        res[name] = {"workload": desc, "bytes": n, "kernel_ms": round(ms, 4),
-                     "input_GBps": round(n / ms / 1e6, 1), "achieved_GBps": round(algo / ms / 1e6, 1),
-                     "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "tokens_per_byte": round(tok / n, 4),
+        res[name] = {"workload": desc + (" (the whole stream on one GPU)" if name == "cfg5" else ""), "bytes": n,
+                     "kernel_ms": round(ms, 4), "input_GBps": round(n / ms / 1e6, 1),
+                     "achieved_GBps": round(algo / ms / 1e6, 1), "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4),
+                     "tokens_per_byte": round(tok / n, 4),
                      "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
-        del d_in, d_out
+        del d_in, d_out, got, exp, host
         s.close()
-    res["multi"] = general_map_rate(blt_amd, synth, O, threads)
+    for name in ("multi", "wrap", "selfval", "chain"):
+        if only and name not in only:
+            continue
+        res[name] = general_map_rate(blt_amd, synth, O, threads, name)
     return res
 
 
-# f2: a general map that needs more than one pass (chained and byte-valued merges, SURVEY.md §8a
-# row f2): one byte pass, then u16 passes until the chain provably stops.
-MULTI_MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
+def general_workload(synth, name):
+    """(host bytes, strategy factory, merges for the oracle, description) of an f2 workload."""
+    import blt_amd
+    if name == "multi":
+        m = synth.CHAINED_TEXT_MAP
+        return synth.text(256 << 20, seed=2), lambda: blt_amd.BpeStrategy(m), m, \
+            "f2: 256 MiB synthetic text (cfg2's), chained + byte-valued 6-entry map, --chunksize 16MB"
+    if name == "selfval":
+        m = synth.SELF_VALUED_MAP
+        return synth.text(256 << 20, seed=2), lambda: blt_amd.BpeStrategy(m), m, \
+            "f2: 256 MiB synthetic text, 4 merges two of which are valued their own first byte (generic byte pass)"
+    if name == "chain":
+        m = synth.doubling_chain(24)
+        return np.full(256 << 20, 97, np.uint8), lambda: blt_amd.BpeStrategy(m), m, \
+            "f2: 256 MiB of 'a', a 24-level doubling chain: 16 MiB chunks become one token each after 24 passes"
+    # wrap: the 65 537-line merges file through the loader
+    import tempfile
+    fd, path = tempfile.mkstemp(suffix=".txt")
+    with os.fdopen(fd, "w") as f:
+        f.write(synth.wrap_merges_lines())
+    m = O_load(path)
+    strat = blt_amd.BpeStrategy.from_file(path)
+    os.unlink(path)
+    return synth.text(256 << 20, seed=2), lambda: strat, m, \
+        "f2: 256 MiB synthetic text, the 65 537-line merges file whose u16 ids wrap (65 536-entry map, L2 buckets)"
 
 
-def general_map_rate(blt_amd, synth, O, threads, reps=10):
-    """256 MiB of cfg2's text through the chained map, device-resident; the timed region is the
-    whole encode_device call (byte pass, u16 passes, the host's read of the pass count)."""
+def O_load(path):
+    from oracle import oracle as O
+    return O.load_bpe_merges_from_path(path)
+
+
+def general_map_rate(blt_amd, synth, O, threads, name="multi", reps=10):
+    """A general map, device-resident; the timed region is the whole encode_device call (byte
+    pass, u16 passes, the host's read of the pass count)."""
     import torch
-    host = synth.text(256 << 20, seed=2)
+    host, make, merges, desc = general_workload(synth, name)
     n = host.size
-    s = blt_amd.BpeStrategy(MULTI_MAP)
+    s = make()
     d_in = torch.from_numpy(host).cuda()
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     wsb = s.workspace_size(n, CHUNK)
@@ -161,14 +220,74 @@ def general_map_rate(blt_amd, synth, O, threads, reps=10):
     ms = float(np.median(ts))
     passes = int(blt_amd._lib.lib().blt_debug_last_u16_passes())
     got = d_out[:2 * tok].cpu().numpy()
-    exp = O.COracle(MULTI_MAP).run(host, CHUNK, threads=threads)
+    exp = O.COracle(merges).run(host, CHUNK, threads=threads)
     algo = n + 2 * tok
     s.close()
-    return {"workload": "f2: 256 MiB synthetic text (cfg2's), chained + byte-valued 6-entry map, --chunksize 16MB",
-            "bytes": n, "ms": round(ms, 4), "u16_passes": passes, "input_GBps": round(n / ms / 1e6, 1),
-            "achieved_GBps": round(algo / ms / 1e6, 1), "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4),
-            "tokens_per_byte": round(tok / n, 4),
+    return {"workload": desc, "bytes": n, "ms": round(ms, 4), "u16_passes": passes,
+            "input_GBps": round(n / ms / 1e6, 1), "achieved_GBps": round(algo / ms / 1e6, 1),
+            "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "tokens_per_byte": round(tok / n, 4),
             "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
+
+
+def cli_end_to_end(synth, host, merges, exp):
+    """The `blt` binary on cfg3's bytes as a tmpfs file to a tmpfs output (--type text), best of 3
+    after one warm run; output bytes checked against the oracle's stream."""
+    import subprocess
+    import tempfile
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    d = tempfile.mkdtemp(prefix="blt_bench_cli_", dir=base)
+    fin, fout, fm = os.path.join(d, "in.txt"), os.path.join(d, "out.bin"), os.path.join(d, "merges.txt")
+    try:
+        host.tofile(fin)
+        with open(fm, "w") as f:
+            f.write("".join(f"{a} {b}\n" for (a, b), _ in sorted(merges.items(), key=lambda kv: kv[1])))
+        cmd = [os.path.join(ROOT, "blt_amd", "blt"), "-i", fin, "-o", fout, "--merges", fm, "--chunksize", "16MB",
+               "--type", "text", "--gpus", "1"]
+        subprocess.run(cmd, check=True, timeout=120)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            subprocess.run(cmd, check=True, timeout=120)
+            ts.append(time.perf_counter() - t0)
+        got = np.fromfile(fout, dtype=np.uint8)
+        ok = bool(got.size == exp.size + 2 and got[0] == 0xFF and got[1] == 0x01 and np.array_equal(got[2:], exp))
+        dt = min(ts)
+        return {"value": round(host.size / dt / 1e9, 3), "unit": "GB/s", "seconds": round(dt, 4),
+                "seconds_all": [round(t, 4) for t in ts], "bytes": int(host.size), "tmpfs": base,
+                "path": "blt -i IN -o OUT --merges M --chunksize 16MB --type text --gpus 1 (process start to exit: "
+                        "merges load, mmap, H2D, kernel, D2H, write)",
+                "bit_exact_vs_oracle": ok}
+    finally:
+        for f in (fin, fout, fm):
+            if os.path.exists(f):
+                os.remove(f)
+        os.rmdir(d)
+
+
+def kernel_source_sha():
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("bpe_kernels.hip", "bpe_kernels.h"):
+        with open(os.path.join(ROOT, "blt_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def pmc_traffic(path, wl, n):
+    """HBM bytes per launch from the PMC record, only if it names this workload, size, chunk size and
+    the kernel source it was measured on."""
+    if not os.path.exists(path):
+        return None, "no record"
+    with open(path) as f:
+        tj = json.load(f)
+    tw = tj.get("workloads", {}).get(wl, {})
+    if not tw:
+        return None, f"no {wl} record"
+    if tw.get("bytes_per_gpu") != n or tw.get("chunk_size") != CHUNK:
+        return None, "record is for another size"
+    if tw.get("kernel_source_sha256") != kernel_source_sha():
+        return None, "record is for another kernel build (kernel_source_sha256 differs)"
+    return tw.get("hbm_bytes_per_launch"), tw.get("source")
 
 
 def host_paths(blt_amd, strategy, host, exp):
@@ -264,15 +383,13 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    n = args.bytes_per_gpu
-    wl_host, merges, wl_desc = workload(synth, args.workload, n)
+    wl = args.workload or ("cfg3" if world == 1 else "cfg4")
+    if wl == "cfg2" and distributed:
+        raise SystemExit("cfg2 is a one-GPU workload")
+    host, merges, wl_desc, (b0, b1), stream_bytes = workload(synth, wl, rank, world, args.bytes_per_gpu,
+                                                             args.total_bytes)
     strategy = blt_amd.BpeStrategy(merges)
-    if wl_host is None:
-        b0, b1 = shard.rank_bytes(world * n, CHUNK, rank, world)   # this rank's chunk range of the stream
-        host = synth.text(b1 - b0, seed=3, offset=b0)
-    else:
-        host = wl_host
-        n = host.size
+    n = host.size
     d_in = torch.from_numpy(host).to("cuda")
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     nchunks = (n + CHUNK - 1) // CHUNK
@@ -312,18 +429,14 @@ def main():
     tokens = int(d_off[-1].item())
 
     elapsed, kern_ms_max = shard.max_over_ranks([elapsed, kern_ms], device="cuda" if backend == "nccl" else None)
+    ranges = shard.gather_ranges((b0, b1), device="cuda" if backend == "nccl" else None)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * n / (elapsed / args.steps) / 1e9
+    total_bytes = sum(r1 - r0 for r0, r1 in ranges)           # bytes all ranks processed per step
+    value = total_bytes / (elapsed / args.steps) / 1e9
 
     algo_bytes = n + 2 * tokens                               # N + 2M per launch
     achieved = algo_bytes / (kern_ms / 1000.0) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic):
-        with open(args.traffic) as f:
-            tj = json.load(f)
-        tw = tj.get("workloads", {}).get(args.workload, {})
-        if tw.get("bytes_per_gpu") == n and tw.get("chunk_size") == CHUNK:
-            traffic = tw.get("hbm_bytes_per_launch")
+    traffic, traffic_src = pmc_traffic(args.traffic, wl, n)
 
     cpu = None
     cpu_opt = None
@@ -346,38 +459,44 @@ def main():
         cpu_s = time.perf_counter() - c0
         cpu = {"value": round(n / cpu_s / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
                "usable_cores": usable, "affinity_cpus": affinity, "os_cpu_count": ncpu,
-               "sample": f"the same {n >> 20} MiB {args.workload} shard, {nchunks} chunks of 16 MiB, C restatement "
+               "sample": f"the same {n >> 20} MiB {wl} shard, {nchunks} chunks of 16 MiB, C restatement "
                          f"of tokenizer.rs:56-93 (hash map, multi-pass), one task per chunk on {threads} threads "
-                         f"(every usable core: cgroup quota, else affinity mask, as num_cpus)",
+                         f"(every usable core: min(cgroup quota, affinity mask), as num_cpus)",
                "seconds": round(cpu_s, 3)}
         got = d_out[:2 * tokens].cpu().numpy()
         exact = bool(exp.size == got.size and np.array_equal(exp, got))
+        del got
         # SURVEY.md §8(d)'s "optimised CPU" line beside it: dense table, one greedy pass per chunk
         c0 = time.perf_counter()
         fast = O.fast_run(merges, host, CHUNK, threads=threads)
         fast_s = time.perf_counter() - c0
         if fast is not None:
             cpu_opt = {"value": round(n / fast_s / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port-optimized",
-                       "sample": f"the same {n >> 20} MiB {args.workload} shard: dense 64K-entry table, one greedy "
+                       "sample": f"the same {n >> 20} MiB {wl} shard: dense 64K-entry table, one greedy "
                                  f"pass per chunk (single-pass map), {threads} threads", "seconds": round(fast_s, 3),
                        "matches_port": bool(np.array_equal(fast, exp))}
-        if not args.no_extra and args.workload == "cfg3":
+        del fast
+        if not args.no_extra and wl == "cfg3":
             del d_in, d_out, ws
-            extras["configs"] = extra_configs(blt_amd, synth, O, threads)
-            extras["end_to_end"], extras["per_chunk_path"] = host_paths(blt_amd, strategy, host, exp)
+            only = tuple(x for x in args.only_configs.split(",") if x)
+            extras["configs"] = extra_configs(blt_amd, synth, O, threads, only)
+            if not only:
+                extras["end_to_end"], extras["per_chunk_path"] = host_paths(blt_amd, strategy, host, exp)
+                extras["cli_end_to_end"] = cli_end_to_end(synth, host, merges, exp)
 
     if rank == 0:
+        strong = wl in STRONG_TOTAL
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": ("synthetic: seeded uniform random bytes (splitmix64), cfg3's merges" if args.workload == "cfg5" else
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "u8",
+            "data": ("synthetic: seeded uniform random bytes (splitmix64), cfg3's merges" if wl == "cfg5" else
                      "synthetic: seeded English-like text (splitmix64, 1 MiB blocks), merges ranked from it"),
-            "config": {"workload": wl_desc,
-                       "bytes_per_gpu": n, "chunk_size": CHUNK, "merges": len(merges),
-                       "parallelism": f"chunk-sharded x{world}, no collective"},
+            "config": {"workload": wl_desc, "stream_bytes": stream_bytes, "bytes_per_gpu": n,
+                       "rank_bytes": [[int(r0), int(r1)] for r0, r1 in ranges], "chunk_size": CHUNK,
+                       "merges": len(merges), "parallelism": f"chunk-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "seg::scan_bytes_kernel<true, true>", "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": algo_bytes},

@@ -23,6 +23,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -184,11 +185,22 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
     int wrc = 0;
     std::string wmsg;
     int rc = 0;
+    // BLT_CLI_TIMING: time in the tokenising calls and waiting for the writer, per run
+    const bool timing = getenv("BLT_CLI_TIMING") != nullptr;
+    double t_tok = 0, t_wait = 0;
+    auto now = [] {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+    };
     for (size_t off = 0, k = 0; off < n && !rc; off += win, ++k) {
         const size_t len = std::min(win, n - off);
         Buf& out = buf[k & 1];
+        const double t0 = timing ? now() : 0;
         rc = st.window(in + off, len, cs, out);
+        const double t1 = timing ? now() : 0;
         if (writer.joinable()) writer.join();   // window k-1 written: its buffer is free
+        if (timing) { t_tok += t1 - t0; t_wait += now() - t1; }
         if (wrc) break;
         if (rc) break;
         writer = std::thread([&sink, &out, &wrc, &wmsg] {
@@ -196,7 +208,15 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
             if (wrc) wmsg = last_error();
         });
     }
-    if (writer.joinable()) writer.join();
+    {
+        const double t1 = timing ? now() : 0;
+        if (writer.joinable()) writer.join();
+        if (timing) {
+            t_wait += now() - t1;
+            fprintf(stderr, "blt timing: %zu window(s) of %zu MiB: tokenise %.4f s, wait for writer %.4f s\n",
+                    (n + win - 1) / win, win >> 20, t_tok, t_wait);
+        }
+    }
     if (rc) return rc;
     if (wrc) return set_error(wrc, "%s", wmsg.c_str());
     return 0;

@@ -25,20 +25,30 @@
 // staged through LDS, with 16-byte coalesced stores.  HBM traffic is one read of the input and
 // one write of the output.
 //
-// Byte-pair map (every map loaded from a merges file): the 64K-entry u16 value table lives in
-// LDS (128 KiB of the CU's 160 KiB), XOR-swizzled so English-text lookups spread over the 32
-// banks.  General u16 maps (chained merges, byte-valued merges, u16 wrap) run extra passes on
-// u16 tokens with an open-addressing table in global memory.
+// Byte pass (every map loaded from a merges file, and pass 1 of every other map; seg::
+// scan_bytes_kernel): the self-token table (entry (a, b) = the merged token, or a itself) lives in
+// LDS as 256 rows of 258 u16 entries (129 KiB of the CU's 160 KiB); the 2-entry row pad skews rows
+// across the banks and the entry address is one v_dot2_u32_u16 of the byte pair.  General u16
+// maps (chained merges, byte-valued merges, u16 wrap) run extra passes on big-endian u16 tokens
+// (seg::scan_tokens_kernel) with a bucket table of the map: one-probe (up to 512 keys) or
+// 2-choice cuckoo buckets, in LDS up to 48 KiB, else read through L2.  merge_pass_kernel /
+// merge_tokens_kernel below are the barrier-phased generic passes for what those two cannot take
+// (byte maps with a merge whose value is its own first byte, chunks under 4 KiB, u16 passes over
+// chunks under 1024 tokens).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <atomic>
+#include <mutex>
+#include <unordered_map>
 
 #include "bpe_kernels.h"
 
 namespace blt {
 
-constexpr int kThreads = 512;                 // 8 waves; 1 workgroup per CU (LDS-bound)
+constexpr int kThreads = 512;                 // generic passes: 8 waves per workgroup; the byte
+                                              // table (128 KiB) allows one per CU, the u16 bucket
+                                              // table (<= 48 KiB) several
 constexpr int kWaves = kThreads / 64;
 constexpr int kSeg = 16;                      // positions per lane per sub-tile
 constexpr int kSubPos = kThreads * kSeg;      // 8192 positions per sub-tile
@@ -2147,6 +2157,30 @@ static int grid_for(uint32_t ntiles, int device, const void* fn, int threads, in
     return (int)(g < 1 ? 1 : g);
 }
 
+// The same for a kernel whose occupancy depends on its dynamic LDS (the u16 pass with the map's
+// bucket table in LDS): cached per (device, kernel, bytes), so a chain of passes queries once.
+static std::mutex g_grid_mu;
+static std::unordered_map<uint64_t, int> g_grid_smem;
+static int grid_for_smem(uint32_t ntiles, int device, const void* fn, int threads, size_t smem) {
+    const uint64_t key = ((uint64_t)(uint32_t)device << 40) ^ ((uint64_t)(uintptr_t)fn << 20) ^ (uint64_t)smem;
+    int g = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_grid_mu);
+        auto it = g_grid_smem.find(key);
+        if (it != g_grid_smem.end()) g = it->second;
+    }
+    if (!g) {
+        int cus = 0, occ = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, smem) != hipSuccess || occ < 1) occ = 1;
+        g = cus * occ;
+        std::lock_guard<std::mutex> lk(g_grid_mu);
+        g_grid_smem[key] = g;
+    }
+    if ((uint64_t)g > ntiles) g = (int)ntiles;
+    return g < 1 ? 1 : g;
+}
+
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s) {
     if (p.ntiles == 0) return hipSuccess;
     if (!input_u16) {
@@ -2161,12 +2195,8 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
     // input size allows; the kernel reads the actual count from p.n_dev.
     const bool lds = p.hbytes <= kHashLdsMax;
     const void* fn = lds ? (const void*)merge_tokens_kernel<true> : (const void*)merge_tokens_kernel<false>;
-    int cus = 0, occ = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 1;
     const size_t smem = lds ? p.hbytes : 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kThreads, smem) != hipSuccess || occ < 1) occ = 1;
-    long long grid = (long long)cus * occ;
-    if (grid > (long long)p.ntiles) grid = p.ntiles;
+    const int grid = grid_for_smem(p.ntiles, device, fn, kThreads, smem);
     if (lds) hipLaunchKernelGGL((merge_tokens_kernel<true>), dim3((unsigned)grid), dim3(kThreads), smem, s, p);
     else hipLaunchKernelGGL((merge_tokens_kernel<false>), dim3((unsigned)grid), dim3(kThreads), 0, s, p);
     return hipGetLastError();

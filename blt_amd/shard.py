@@ -51,6 +51,18 @@ def max_over_ranks(values: Sequence[float], device=None) -> List[float]:
     return [float(v) for v in t.cpu()]
 
 
+def gather_ranges(rng: Tuple[int, int], device=None) -> List[Tuple[int, int]]:
+    """Every rank's (b0, b1), in rank order (this rank's alone without a process group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return [tuple(int(x) for x in rng)]
+    t = torch.tensor(list(rng), dtype=torch.int64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [(int(a), int(b)) for a, b in (o.cpu().tolist() for o in out)]
+
+
 def run_sharded(data: np.ndarray, chunk_size: int, process: Callable[[np.ndarray], Tuple[np.ndarray, np.ndarray]],
                 gather: bool = True) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray], Optional[np.ndarray]]:
     """Tokenises this rank's shard with process(shard) -> (tokens_be_bytes, chunk_lens) and, with

@@ -7,6 +7,11 @@
   as merges-file lines: cfg2 uses k = 256.
 * ``text_merges_50k(data, seed)`` — every pair seen in the text by frequency, then the remaining
   pairs in a seeded permutation, up to 50 000 lines (cfg3/cfg4/cfg5).
+* General maps of SURVEY.md §8 row f2 (several passes, tokenizer.rs:63-86): ``CHAINED_TEXT_MAP``
+  (chained and byte-valued merges on text), ``SELF_VALUED_MAP`` (merges whose value is their own
+  first byte, which only the generic byte pass takes), ``doubling_chain(depth)`` (one pass per
+  level over runs of one byte), ``wrap_merges_lines()`` (a 65 537-line merges file whose u16 ids
+  wrap, config_loader.rs:18, :40).
 
 Streams are generated in independent 1 MiB blocks, so ``offset`` selects any slice of a longer
 stream (each rank of a multi-GPU run generates only its shard).
@@ -91,3 +96,23 @@ def merges_dict(pairs: List[Tuple[int, int]]) -> Dict[Tuple[int, int], int]:
     for i, (a, b) in enumerate(pairs):
         d[(a, b)] = (256 + i) & 0xFFFF
     return d
+
+
+# f2 workloads (general maps: a byte pass, then u16 passes until one merges nothing)
+CHAINED_TEXT_MAP = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
+# "e " -> e and "th" -> t (value = its own first byte: the self-token byte kernel cannot take it),
+# "in" -> 256, then "in" "g" -> 257
+SELF_VALUED_MAP = {(101, 32): 101, (116, 104): 116, (105, 110): 256, (256, 103): 257}
+
+
+def doubling_chain(depth: int) -> Dict[Tuple[int, int], int]:
+    """(97, 97) -> 256, (256, 256) -> 257, ...: a run of 2^depth 'a' is one token after depth passes."""
+    m = {(97, 97): 256}
+    for k in range(1, depth):
+        m[(255 + k, 255 + k)] = 256 + k
+    return m
+
+
+def wrap_merges_lines() -> str:
+    """Every byte pair in order, then "1 2": 65 537 lines; ids wrap to 0..255 after line 65 280."""
+    return "".join(f"{i >> 8} {i & 255}\n" for i in range(65536)) + "1 2\n"

@@ -115,10 +115,12 @@ int blt_bpe_process_chunk(const blt_bpe *h, const uint8_t *in, size_t n, uint8_t
 
 /* The mmap pipeline for a BPE strategy (pipeline.rs:56-192): split in into chunks of
  * chunk_size bytes (pipeline.rs:73-81), tokenise each chunk independently, concatenate in chunk
- * order.  The chunks form n_gpus shards (contiguous chunk ranges, no collective), one host
- * thread each; shard r runs on device r % (visible devices), so n_gpus above the device count
- * shares devices.  The output is identical for every n_gpus.  chunk_out_len (nullable) receives each chunk's output bytes.
- * out_cap >= 2 * n. */
+ * order.  Windows of whole chunks are dealt round-robin over min(n_gpus, visible devices)
+ * devices (no collective); per device one thread copies windows in and launches their merge
+ * scans while another copies each window's tokens straight to its final offset in out as soon as
+ * every earlier window is counted, so devices overlap and nothing packs the output afterwards.
+ * The output is identical for every n_gpus.  chunk_out_len (nullable) receives each chunk's
+ * output bytes.  out_cap >= 2 * n. */
 int blt_bpe_process_chunks(const blt_bpe *h, const uint8_t *in, size_t n, size_t chunk_size, int n_gpus,
                            uint8_t *out, size_t out_cap, size_t *out_len, uint64_t *chunk_out_len);
 

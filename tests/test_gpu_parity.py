@@ -3,6 +3,7 @@
 Bit-exact everywhere: this is integer/byte work.  Sizes are chosen so the oracle finishes in
 seconds; the full BASELINE sizes are covered in test_gpu_fullsize.py.
 """
+import contextlib
 import random
 
 import numpy as np
@@ -198,17 +199,18 @@ def test_random_bytes_50k_merges():
 @pytest.mark.parametrize("kind", ["text", "random"])
 def test_multi_gpu_shards_bit_exact(n_gpus, kind):
     """The multi-device path of blt_bpe_process_chunks (pipeline.rs:141-168's concurrent tasks):
-    n_gpus shards of contiguous chunk ranges, one host thread each, shard r on device r % count
-    (so on a one-GPU box every shard thread really runs, sharing the device), each writing its
-    worst-case output slot, then the memmove stitch in chunk order.  A chunk count that does not
-    divide evenly, an odd chunk size and a short last chunk; output and per-chunk lengths
-    bit-exact against the oracle."""
+    n_gpus device contexts, context d on device d % count (so on a one-GPU box every context's
+    producer and drain threads really run, sharing the device), windows of whole chunks dealt
+    round-robin, each window's tokens copied straight to its final offset once every earlier
+    window is counted.  A chunk count that does not divide evenly, an odd chunk size and a short
+    last chunk; output and per-chunk lengths bit-exact against the oracle."""
     cs = 262147
     n = 23 * cs + 12345   # 24 chunks: 8 shards of 3, 3 shards of 8, 2 of 12; short last chunk
     data = synth.text(n, seed=40 + n_gpus) if kind == "text" else synth.random_bytes(n, seed=40 + n_gpus)
     m = synth.merges_dict(synth.text_merges_50k(synth.text(4 << 20, seed=4), seed=4))
     s = blt_amd.BpeStrategy(m)
-    got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
+    with shared_contexts():
+        got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
     orc = O.COracle(m)
     exp = orc.run(data, cs, threads=4)
     assert np.array_equal(got, exp)
@@ -216,6 +218,54 @@ def test_multi_gpu_shards_bit_exact(n_gpus, kind):
     assert np.array_equal(lens, elens)
     one = s.process_chunks(data, cs, n_gpus=1)
     assert np.array_equal(one, got)
+
+
+@contextlib.contextmanager
+def shared_contexts():
+    """n_gpus device contexts even on a one-GPU box (blt_debug_set_shared_contexts)."""
+    from blt_amd import _lib
+    _lib.lib().blt_debug_set_shared_contexts(1)
+    try:
+        yield
+    finally:
+        _lib.lib().blt_debug_set_shared_contexts(0)
+
+
+@pytest.mark.parametrize("n_gpus", [1, 2, 5])
+def test_multi_context_many_windows(n_gpus):
+    """More windows per context than it has slots (so slots are reused behind their drains), an
+    odd chunk size, a short last chunk: 300 MiB + 777 B of text in 1 MiB + 3 B chunks (31 chunks
+    per window)."""
+    cs = (1 << 20) + 3
+    n = (300 << 20) + 777
+    data = synth.text(n, seed=77)
+    m = synth.merges_dict(synth.text_merges_50k(synth.text(4 << 20, seed=4), seed=4))
+    s = blt_amd.BpeStrategy(m)
+    with shared_contexts():
+        got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
+    exp = O.COracle(m).run(data, cs, threads=8)
+    assert np.array_equal(got, exp)
+    assert int(lens.sum()) == got.size and lens.size == (n + cs - 1) // cs
+    # by default contexts that would share a device are one context per device
+    assert np.array_equal(s.process_chunks(data, cs, n_gpus=n_gpus), exp)
+
+
+@pytest.mark.parametrize("n_gpus", [2, 3])
+def test_multi_context_general_map(n_gpus):
+    """A general map (byte pass + u16 passes, chained on each context's device) over n_gpus
+    contexts: one window per context, stitched in chunk order."""
+    cs = 262147
+    n = 23 * cs + 12345
+    data = synth.text(n, seed=91)
+    m = {(101, 32): 256, (256, 116): 257, (116, 104): 65, (65, 101): 258, (32, 116): 259, (259, 104): 260}
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    with shared_contexts():
+        got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
+    orc = O.COracle(m)
+    assert np.array_equal(got, orc.run(data, cs, threads=4))
+    elens = np.array([len(orc.process_chunk(data[k * cs:(k + 1) * cs].tobytes())) for k in range(24)])
+    assert np.array_equal(lens, elens)
 
 
 def test_sticky_device_error():

@@ -3,7 +3,8 @@
     python tools/host_path_rate.py [--mib 1024]
 
 1. cfg3 through the host-buffer entry point blt_bpe_process_chunks (pageable host input ->
-   device -> host output, chunk lengths): the PCIe-inclusive rate.  Never the bench value.
+   device -> host output, chunk lengths) at each --gpus n_gpus (device contexts; on a one-GPU box
+   they share the device): the PCIe-inclusive rate.  Never the bench value.
 2. cfg2 (256 merges, 100 MiB text, 16 MiB chunks) on device-resident buffers: kernel rate and
    output tokens per input byte.
 Both outputs are checked bit-exactly against the C oracle.
@@ -46,6 +47,9 @@ def device_rate(strategy, host, cs, reps=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=1024)
+    ap.add_argument("--gpus", default="1,8", help="n_gpus values for blt_bpe_process_chunks (contexts; on a one-GPU "
+                                                   "box they share the device)")
+    ap.add_argument("--no-cfg2", action="store_true")
     a = ap.parse_args()
     import blt_amd
     from blt_amd import synth
@@ -56,13 +60,37 @@ def main():
     m3 = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
     s3 = blt_amd.BpeStrategy(m3)
     text = synth.text(n, seed=3)
-    s3.process_chunks(text[:1 << 20], CHUNK)       # warm the device tables
-    t0 = time.perf_counter()
-    out = s3.process_chunks(text, CHUNK)
-    dt = time.perf_counter() - t0
     exp = O.COracle(m3).run(text, CHUNK, threads=16)
-    res["cfg3_host_path"] = {"bytes": n, "seconds": round(dt, 4), "GBps": round(n / dt / 1e9, 3),
-                             "bit_exact": bool(np.array_equal(out, exp))}
+    import ctypes
+    from blt_amd import _lib
+    L = _lib.lib()
+    out = np.empty(2 * n, np.uint8)   # one caller buffer, first-touched by the warm call
+    olen = ctypes.c_size_t(0)
+    runs = [(int(x), False) for x in a.gpus.split(",")]
+    runs += [(g, True) for g, _ in runs if g > 1]   # n_gpus contexts sharing the one device
+    for g, shared in runs:
+        L.blt_debug_set_shared_contexts(1 if shared else 0)
+
+        def call():
+            _lib.check(L.blt_bpe_process_chunks(s3.handle, text.ctypes.data, n, CHUNK, g, out.ctypes.data, out.size,
+                                                ctypes.byref(olen), None))
+        call()       # device tables, context buffers
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        dt = min(ts)
+        L.blt_debug_set_shared_contexts(0)
+        res[f"cfg3_host_path_n_gpus{g}" + ("_shared_contexts" if shared else "")] = {
+                                            "bytes": n, "n_gpus": g, "contexts": g if shared else 1,
+                                            "seconds": round(dt, 4),
+                                            "seconds_all": [round(t, 4) for t in ts],
+                                            "GBps": round(n / dt / 1e9, 3),
+                                            "bit_exact": bool(np.array_equal(out[:olen.value], exp))}
+    if a.no_cfg2:
+        print(json.dumps(res))
+        return
 
     t2 = synth.text(100 << 20, seed=2)
     m2 = synth.merges_dict(synth.top_pair_merges(t2, 256))

@@ -85,12 +85,19 @@ def main():
         result["hbm_bytes_per_launch"] = int((2.0 * pd["FETCH_SIZE"] + pd["WRITE_SIZE"]) * 1024)
         result["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 FETCH_SIZE counts half of wide reads"
         # what bench.py reports as roofline.traffic for the same workload
-        n = GIB
+        n, wl = GIB, "cfg3"
         for i, x in enumerate(bench_args):
             if x == "--bytes-per-gpu":
                 n = int(bench_args[i + 1])
+            if x == "--workload":
+                wl = bench_args[i + 1]
+            if x == "--total-bytes":
+                n = int(bench_args[i + 1])
+        sys.path.insert(0, ROOT)
+        import bench
         with open(os.path.join(a.outdir, "traffic.json"), "w") as f:
-            json.dump({"bytes_per_gpu": n, "chunk_size": CHUNK, "kernel": a.kernel,
+            json.dump({"workload": wl, "bytes_per_gpu": n, "chunk_size": CHUNK, "kernel": a.kernel,
+                       "kernel_source_sha256": bench.kernel_source_sha(),
                        "hbm_bytes_per_launch": result["hbm_bytes_per_launch"], "note": result["traffic_note"]}, f,
                       indent=1)
     with open(os.path.join(a.outdir, "pmc_summary.json"), "w") as f:

@@ -60,6 +60,13 @@ def main():
               f"table copied p50 {np.median(us_(wg[:, 1])):.2f} max {us_(wg[:, 1]).max():.2f}; "
               f"exit p50 {np.median(us_(wg[:, 2])):.2f} max {us_(wg[:, 2]).max():.2f}; "
               f"tile publishes first {us_(pubs.min()):.2f} last {us_(pubs.max()):.2f}")
+        ex = np.sort(us_(wg[:, 2]))
+        print("  exit us percentiles p0 %.2f p10 %.2f p50 %.2f p90 %.2f p100 %.2f; start p0 %.2f p100 %.2f" %
+              (ex[0], np.percentile(ex, 10), np.median(ex), np.percentile(ex, 90), ex[-1],
+               us_(wg[:, 0]).min(), us_(wg[:, 0]).max()))
+        ps = np.sort(us_(pubs))
+        print("  tile publishes: first 256 done by %.2f us, last 256 start at %.2f us; mean gap per 256 tiles %.3f us" %
+              (ps[min(255, ps.size - 1)], ps[max(0, ps.size - 256)], (ps[-1] - ps[0]) / max(1, ps.size / 256)))
     how = rec[1:4 * ntiles:4] & 0xFFFFFFFF
     wv8 = rec[8 * ntiles:(8 + 8 * 16) * ntiles].reshape(ntiles, 16, 8)
     wv = wv8[:, :, :6]
