@@ -497,7 +497,7 @@ def main():
                        "merges": len(merges), "parallelism": f"chunk-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "seg::scan_bytes_kernel<true, true>", "kernel_ms": round(kern_ms, 4),
+                         "kernel": "seg::scan_bytes_kernel<true, 0, false>", "kernel_ms": round(kern_ms, 4),
                          "kernel_ms_max_rank": round(kern_ms_max, 4),
                          "algorithmic_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,

@@ -248,11 +248,17 @@ struct blt_bpe {
     uint32_t sentinel = 0;                 // > 0xFFFF: every byte pair is a merge
     std::vector<uint16_t> dense;           // 65536, swizzled (blt::dense_index)
     // Self-token tables of the byte-pass kernel: entry (a, b) = merged token, or a itself when
-    // (a, b) is no merge.  Usable when no byte-pair key (a, b) maps to a (self_ok).
-    bool self_ok = true;
-    // Every byte-pair merge value is >= 256 (every merges file: ids 256 + line): the byte-pass
-    // kernel then reads "merge" off the entry's high byte instead of comparing it with a.
-    bool hi_merge = true;
+    // (a, b) is no merge.  byte_mode, the kernel's merge test (launch_scan_bytes): 0 every byte-pair
+    // merge value is >= 256 (every merges file: ids 256 + line), so "merge" is the entry's high
+    // byte; 1 the entry differs from a; 2 as 1, with merges valued their own first byte a stored as
+    // (mark << 8) | a, mark a high byte no merge value has; -1 none applies (the generic byte pass).
+    // allmerge: every byte pair is a merge (the test is skipped).
+    int byte_mode = 0;
+    bool allmerge = false;
+    uint32_t mark = 0;
+    // A general map whose keys are all byte pairs: its first pass reports whether it made a token
+    // below 256 (the only key components), and is the fixpoint when it made none.
+    bool live_first = false;
     std::vector<uint16_t> self_ne, self_be;
     // General map (not single_pass): 2-choice cuckoo table of one-slot buckets for the u16 passes
     // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31
@@ -400,16 +406,37 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
         if (a < 256 && b < 256) h->dense[blt::dense_index(a, b)] = kv.second;
     }
     auto bswap = [](uint32_t v) { return (uint16_t)(((v & 0xFF) << 8) | ((v >> 8) & 0xFF)); };
+    bool hi_merge = true, self_valued = false, byte_keys = true;
+    std::vector<uint8_t> hi_used(256, 0);   // high bytes of byte-pair merge values
+    for (const auto& kv : map) {
+        const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
+        if (a < 256 && b < 256) {
+            if (kv.second == a) self_valued = true;
+            if (kv.second < 256) hi_merge = false;
+            hi_used[kv.second >> 8] = 1;
+        } else {
+            byte_keys = false;
+        }
+    }
+    h->allmerge = byte_pairs == 65536;
+    if (hi_merge) {
+        h->byte_mode = 0;
+    } else if (!self_valued || h->allmerge) {
+        h->byte_mode = 1;
+    } else {
+        h->byte_mode = -1;
+        for (uint32_t m = 1; m < 256 && h->byte_mode < 0; ++m)
+            if (!hi_used[m]) { h->byte_mode = 2; h->mark = m; }
+    }
+    h->live_first = !h->single_pass && byte_keys && h->byte_mode > 0;
     h->self_ne.assign(blt::kSelfEntries, 0);
     for (uint32_t a = 0; a < 256; ++a)
         for (uint32_t b = 0; b < 256; ++b) h->self_ne[blt::self_index(a, b)] = (uint16_t)a;
     for (const auto& kv : map) {
         const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
-        if (a < 256 && b < 256) {
-            h->self_ne[blt::self_index(a, b)] = kv.second;
-            if (kv.second == a) h->self_ok = false;
-            if (kv.second < 256) h->hi_merge = false;
-        }
+        if (a < 256 && b < 256)
+            h->self_ne[blt::self_index(a, b)] = (h->byte_mode == 2 && kv.second == a) ? (uint16_t)((h->mark << 8) | a)
+                                                                                     : kv.second;
     }
     h->self_be.resize(blt::kSelfEntries);
     for (uint32_t i = 0; i < blt::kSelfEntries; ++i) h->self_be[i] = bswap(h->self_ne[i]);
@@ -557,7 +584,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
              uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr,
              bool tok_scan = false) {
-    const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->self_ok;   // byte-pass fast kernel
+    const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->byte_mode >= 0 && be;   // byte-pass fast kernel
     const uint64_t tile = columnar ? blt::kTilePosBytes
                                    : in_u16 ? (tok_scan ? blt::kTilePosTok : blt::kTilePosU16) : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
@@ -595,10 +622,12 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
         p.cs_tiles = (uint32_t)(cs / blt::kTilePosBytes);
         p.cs_tiles_magic = p.cs_tiles > 1 ? (uint32_t)(0xFFFFFFFFull / p.cs_tiles) : 0u;
     }
+    p.allm = h->allmerge ? 1u : 0u;
+    p.mark = h->mark | (h->mark << 16);
     p.debug = g_debug_tiles;
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
-    if (columnar) HIP_TRY(blt::launch_scan_bytes(p, be ? 1 : 0, h->hi_merge ? 1 : 0, dev, s));
+    if (columnar) HIP_TRY(blt::launch_scan_bytes(p, h->byte_mode, (chain && h->live_first) ? 1 : 0, dev, s));
     else if (in_u16 && tok_scan) HIP_TRY(blt::launch_scan_tokens(p, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
@@ -655,8 +684,11 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // pass 1's control block and status words and the chain's totals are contiguous: one memset
     // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
     HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + 32, s));
-    if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0], true))
-        return rc;
+    {   // pass 1 (pass id 0): with byte-pair keys it marks itself final when it made no key component
+        const Chain c0{nullptr, tot, done, 0};
+        if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0], true, &c0))
+            return rc;
+    }
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
@@ -685,8 +717,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if ((uint32_t)rec[2]) break;
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
-    t_last_u16_passes = (uint32_t)rec[2];
-    const uint32_t last = (uint32_t)rec[2] & 1u;   // the arrays the final pass wrote
+    const uint32_t kdone = (uint32_t)rec[2] & ~blt::kDoneBytePass;   // 0: pass 1 was final
+    t_last_u16_passes = kdone;
+    const uint32_t last = kdone & 1u;   // the arrays the final pass wrote
     if (d_chunk_off && off[last] != d_chunk_off)
         HIP_TRY(hipMemcpyAsync(d_chunk_off, off[last], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
     if (out_tokens) *out_tokens = rec[last];
@@ -1231,6 +1264,13 @@ int blt_bpe_check_workspace(void* d_ws, void* stream) {
         return fail(rc, "%s", msg.c_str());
     }
     return 0;
+}
+
+// Not in the public header: the handle's byte-pass choice (tests): byte_mode (-1: the generic byte
+// pass) in the low byte, allmerge << 8, live_first << 9.
+int blt_debug_byte_mode(const blt_bpe* h) {
+    if (!h) return -1;
+    return (h->byte_mode & 0xFF) | (h->allmerge ? 0x100 : 0) | (h->live_first ? 0x200 : 0);
 }
 
 // Not in the public header: a test hook that makes blt_bpe_process_chunks run n_gpus device

@@ -55,6 +55,9 @@ struct PassParams {
     uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles
                                // (below 2^31), else 0
     uint32_t cs_tiles_magic;   // floor((2^32 - 1) / cs_tiles) (cs_tiles > 1)
+    uint32_t allm;             // byte pass: every byte pair is a merge (the entry's test is skipped)
+    uint32_t mark;             // byte pass, mode 2: BE pattern (mark | mark << 16) of the high byte that
+                               // marks a merge valued its own first byte
     uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
                                // error bits in ctl[1], so the handle's next call fails
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
@@ -65,10 +68,15 @@ struct PassParams {
 // Generic pass: byte input with the dense LDS table (maps the byte pass cannot take), or BE u16
 // tokens with the bucket table (p.hbuckets) for the later passes of a general map; output BE.
 hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian, int device, hipStream_t s);
-// Byte-input pass (segment kernel, seg::scan_bytes_kernel): p.cs >= kMinChunkBytes; tiles of
-// kTilePosBytes positions.
-// hi_merge: every byte-pair merge value is >= 256, so an entry's high byte tells a merge.
-hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s);
+// Byte-input pass (segment kernel, seg::scan_bytes_kernel), big-endian output: p.cs >=
+// kMinChunkBytes; tiles of kTilePosBytes positions.  mode: 0 every byte-pair merge value is >= 256,
+// so an entry's high byte tells a merge; 1 an entry that differs from the token of a is a merge; 2
+// as 1 with merges valued their own first byte marked (p.mark).  live (modes 1 and 2): the first
+// pass of a general map whose keys are byte pairs; it sets *p.done = kDoneBytePass when it made no
+// token below 256.
+hipError_t launch_scan_bytes(const PassParams& p, int mode, int live, int device, hipStream_t s);
+// done word value of a byte pass after which nothing merges (u16 pass k writes k)
+constexpr uint32_t kDoneBytePass = 0x80000000u;
 // u16 pass of a general map on the scan kernel (seg::scan_tokens_kernel), in place (p.in may equal
 // p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
 // at least kTokRange tokens.

@@ -605,6 +605,10 @@ __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
     const u16x2 r = __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b);   // v_pk_add_u16
     return __builtin_bit_cast(uint32_t, r);
 }
+__device__ __forceinline__ uint32_t pk_mul(uint32_t a, uint32_t b) {
+    const u16x2 r = __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b);   // v_pk_mul_lo_u16
+    return __builtin_bit_cast(uint32_t, r);
+}
 // Each 16-bit half -> 1 if nonzero, else 0 (the compiler would expand min into compares).
 __device__ __forceinline__ uint32_t pk_nz(uint32_t v) {
     uint32_t r;
@@ -822,10 +826,20 @@ __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t 
 // ---- phase 1 of a tile: lookups, lane functions, wave functions ------------------------------
 // Three straight-line passes over the kS sub-tiles (lookups; the rare uniform fix-up of buffer
 // and chunk ends; lane functions and wave resolves), so the scheduler can overlap sub-tiles.
-template <bool kBE, bool kHiM>
+// kMode (the merge test of a self-token entry): 0 (kHiM) a merge value is >= 256, so "merge" is the
+// entry's high byte; 1 the entry differs from the token of a itself; 2 as 1, and merges valued their
+// own first byte a are stored as (mark << 8) | a (mark: a high byte no merge value has), whose high
+// byte is cleared once the test is done.  allm (uniform): every byte pair is a merge (a merges file
+// listing all 65 536 pairs), whatever the entry.  kLive: the lane also reports whether one of its
+// merges (surviving buffer and chunk ends) made a token below 256, the only key components of a
+// map whose keys are byte pairs: a first pass with none is the fixpoint (see scan_bytes_kernel).
+template <bool kBE, int kMode, bool kLive>
 __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS][4], const uint32_t (&nxt)[kS],
                                             const TInfo& ti, uint32_t cs32, uint32_t wave, int lane,
-                                            TileState& st, uint32_t (*wfn)[4], uint64_t* sub = nullptr) {
+                                            TileState& st, uint32_t (*wfn)[4], uint32_t allm, uint32_t mark,
+                                            uint64_t* sub = nullptr) {
+    static_assert(kBE, "the byte pass writes big-endian tokens");
+    static_assert(kMode >= 0 && kMode <= 2 && !(kLive && kMode == 0), "phase-1 mode");
     uint32_t m[kS];
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
@@ -854,19 +868,23 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             uint32_t d;
-            if (kHiM) {
+            if (kMode == 0) {
                 // a merge is a token >= 256, a itself < 256: the token's high byte (BE: low byte)
-                d = st.v[j][h] & (kBE ? 0x00FF00FFu : 0xFF00FF00u);
+                d = st.v[j][h] & 0x00FF00FFu;
             } else {
-                // token of a itself (positions 2h, 2h+1: bytes 2h, 2h+1 of the lane), in output
-                // byte order: BE (a << 8), native a
+                // token of a itself (positions 2h, 2h+1: bytes 2h, 2h+1 of the lane), BE (a << 8)
                 const uint32_t xw = x[j][h >> 1];
-                const uint32_t self = kBE ? __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x030C020Cu : 0x010C000Cu)
-                                          : __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x0C030C02u : 0x0C010C00u);
+                const uint32_t self = __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x030C020Cu : 0x010C000Cu);
                 d = st.v[j][h] ^ self;
+                if (kMode == 2) {
+                    // a marked entry (BE high byte = mark) is the merge value a: clear the mark
+                    const uint32_t keep = pk_nz((st.v[j][h] ^ mark) & 0x00FF00FFu);   // 1: not marked
+                    st.v[j][h] &= pk_mul(keep, 0x00FF00FFu) | 0xFF00FF00u;
+                }
             }
             m32 |= pk_nz(d) << (2 * h);
         }
+        if (allm) m32 = 0x7FFF7FFFu;
         m[j] = (m32 & 0xFFFFu) | (m32 >> 15);
     }
     // buffer end and chunk ends (uniform per wave range; rare)
@@ -903,11 +921,23 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
             st.mv[j] = m[j] | 0xFFFF0000u;
         }
     }
+    uint32_t wlive = 0;
+    if (kLive) {   // a surviving merge whose token is below 256 (BE high byte 0)
+        uint32_t lv = 0;
+#pragma unroll
+        for (int j = 0; j < kS; ++j) {
+            uint32_t low32 = 0;   // as m32: even positions in bits 0..14, odd in 16..30
+#pragma unroll
+            for (int h = 0; h < 8; ++h) low32 |= (pk_nz(st.v[j][h] & 0x00FF00FFu) ^ 0x00010001u) << (2 * h);
+            lv |= m[j] & ((low32 & 0xFFFFu) | (low32 >> 15));
+        }
+        wlive = __ballot(lv != 0u) != 0 ? 1u : 0u;
+    }
     if (sub) {   // timing build: lookups and masks done
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         sub[0] = __builtin_amdgcn_s_memtime();
     }
-    lane_wave_fns<kS>(m, wave, lane, st, wfn);
+    lane_wave_fns<kS>(m, wave, lane, st, wfn, wlive);
     if (sub) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         sub[1] = __builtin_amdgcn_s_memtime();
@@ -1407,7 +1437,13 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
 // wave's emission (a whole iteration for the device-scope atomic to return).  (Measured: the
 // claiming lane computing the claimed tile's chunk geometry once for all waves and publishing it
 // with the ticket delays the hand-over, and cfg3 loses 2 %.)
-template <bool kBE, bool kHiM>
+//
+// kLive (the first pass of a general map whose keys are all byte pairs): the tiles' live bits (a
+// merge made a token below 256: see phase1_tile) travel with the status words, and the last tile
+// marks the pass final (done = kDoneBytePass) when no tile had one: every later pass would merge
+// nothing (a pair this pass left alone was looked up and rejected; a token >= 256 is in no key),
+// so the u16 passes the host enqueued behind it return at once.
+template <bool kBE, int kMode, bool kLive>
 __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_tab[kSelfEntries];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
@@ -1429,6 +1465,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint64_t n = p.n;
     const uint32_t ntiles = p.ntiles;
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
+    const uint32_t allm = uni(p.allm), mark = uni(p.mark);
 
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
@@ -1501,7 +1538,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             // phase 1 last and so hold back the tile's resolve and aggregate (which successors'
             // look-backs wait for), and finish emission last (which holds back their next phase 1)
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            phase1_tile<kBE, kHiM>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot], stamping ? sub : nullptr);
+            phase1_tile<kBE, kMode, kLive>(tab, x, nxt, ti, cs32, wave, lane, sc, s_wfn[slot], allm, mark,
+                                           stamping ? sub : nullptr);
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
@@ -1509,7 +1547,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             old = uni(old);
             lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                resolve_tile<kGroups, kLive>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
@@ -1526,9 +1564,10 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone, it);
-            const uint32_t tf0 = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
-            const uint32_t tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
+            const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+            const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
             if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live, kTiming ? &bad : nullptr);
+            live |= (tfl >> 1) & 1u;   // tiles up to and including Tp (kLive; 0 otherwise)
             if (lane == 0) {
                 const uint64_t end = O + (C == 1u ? tf3 : tf2);
                 // a failed tile (flagged) writes nothing (C = 2) and publishes a prefix only so its
@@ -1542,11 +1581,12 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                 s_O[pslot] = O;
                 lds_release(&s_lbdone, it + 1u);
                 const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin));
+                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
                     *p.total = fin;
                     if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
+                    if (kLive && p.done && C <= 1u && (fin == n || !live)) *p.done = kDoneBytePass;
                 }
                 if (p.debug) {
                     uint64_t* d = p.debug + 4ull * Tp;
@@ -2202,22 +2242,21 @@ hipError_t launch_merge_pass(const PassParams& p, int input_u16, int big_endian,
     return hipGetLastError();
 }
 
-hipError_t launch_scan_bytes(const PassParams& p, int big_endian, int hi_merge, int device, hipStream_t s) {
+hipError_t launch_scan_bytes(const PassParams& p, int mode, int live, int device, hipStream_t s) {
     if (p.ntiles == 0) return hipSuccess;
-    const void* fn = big_endian ? (hi_merge ? (const void*)seg::scan_bytes_kernel<true, true>
-                                            : (const void*)seg::scan_bytes_kernel<true, false>)
-                                : (hi_merge ? (const void*)seg::scan_bytes_kernel<false, true>
-                                            : (const void*)seg::scan_bytes_kernel<false, false>);
+    using seg::scan_bytes_kernel;
+    const void* fn = mode == 0 ? (const void*)scan_bytes_kernel<true, 0, false>
+                     : mode == 1 ? (live ? (const void*)scan_bytes_kernel<true, 1, true> : (const void*)scan_bytes_kernel<true, 1, false>)
+                                 : (live ? (const void*)scan_bytes_kernel<true, 2, true> : (const void*)scan_bytes_kernel<true, 2, false>);
+    if (mode < 0 || mode > 2 || (mode == 0 && live)) return hipErrorInvalidValue;
     // every byte-pass instantiation holds the whole LDS: one workgroup per CU, one cache entry
     const int grid = grid_for(p.ntiles, device, fn, seg::kThreads, 4);
     const dim3 g((unsigned)grid), b(seg::kThreads);
-    if (big_endian) {
-        if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<true, true>), g, b, 0, s, p);
-        else hipLaunchKernelGGL((seg::scan_bytes_kernel<true, false>), g, b, 0, s, p);
-    } else {
-        if (hi_merge) hipLaunchKernelGGL((seg::scan_bytes_kernel<false, true>), g, b, 0, s, p);
-        else hipLaunchKernelGGL((seg::scan_bytes_kernel<false, false>), g, b, 0, s, p);
-    }
+    if (mode == 0) hipLaunchKernelGGL((scan_bytes_kernel<true, 0, false>), g, b, 0, s, p);
+    else if (mode == 1 && live) hipLaunchKernelGGL((scan_bytes_kernel<true, 1, true>), g, b, 0, s, p);
+    else if (mode == 1) hipLaunchKernelGGL((scan_bytes_kernel<true, 1, false>), g, b, 0, s, p);
+    else if (live) hipLaunchKernelGGL((scan_bytes_kernel<true, 2, true>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((scan_bytes_kernel<true, 2, false>), g, b, 0, s, p);
     return hipGetLastError();
 }
 

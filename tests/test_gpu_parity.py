@@ -715,3 +715,78 @@ def test_random_byte_maps_chunked(seed):
     exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
     assert np.array_equal(got, exp), (seed, alph, density, n, cs)
     assert np.array_equal(lens, elens)
+
+
+def _byte_mode(s):
+    v = blt_amd._lib.lib().blt_debug_byte_mode(s.handle)
+    return {"mode": (v & 0xFF) - (256 if v & 0x80 else 0), "allmerge": bool(v & 0x100), "live": bool(v & 0x200)}
+
+
+def test_byte_pass_self_valued_merges():
+    """Merges valued their own first byte ("e " -> e, "th" -> t) run on the byte pass with marked
+    entries (mode 2), and so does the wrap-around merges file (every pair a merge); a map whose
+    merge values use every high byte has no mark and runs the generic byte pass.  Bit-exact at
+    chunk sizes that cut merges."""
+    text = synth.text((3 << 20) + 77, seed=61)
+    s = blt_amd.BpeStrategy(synth.SELF_VALUED_MAP)
+    assert _byte_mode(s) == {"mode": 2, "allmerge": False, "live": False}   # (256, 103): a u16 key
+    for cs in (1 << 20, 65537, 4096):
+        got, lens = s.process_chunks(text, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(synth.SELF_VALUED_MAP).run(text, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp) and np.array_equal(lens, elens), cs
+    # single-pass self-valued maps on random bytes (values < 256 that are no key component would
+    # make them general; these keys use all bytes, so any value < 256 is a component)
+    rng = random.Random(62)
+    for trial in range(4):
+        keys = {(rng.randrange(256), rng.randrange(256)) for _ in range(3000)}
+        m = {k: (k[0] if rng.random() < 0.2 else 256 + rng.randrange(40000)) for k in keys}
+        s = blt_amd.BpeStrategy(m)
+        assert _byte_mode(s)["mode"] == 2
+        data = np.frombuffer(rng.randbytes((1 << 20) + 13 * trial), np.uint8)
+        got = s.process_chunks(data, 262144 + trial)
+        assert np.array_equal(got, O.COracle(m).run(data, 262144 + trial, threads=8)), trial
+    # every high byte in use: no mark, the generic byte pass
+    m = {(a, 7): (a << 8) | 7 for a in range(1, 256)}
+    m[(0, 0)] = 0
+    s = blt_amd.BpeStrategy(m)
+    assert _byte_mode(s)["mode"] == -1
+    data = np.frombuffer(bytes(random.Random(63).choice([0, 7, 9, 200]) for _ in range(300001)), np.uint8)
+    assert np.array_equal(s.process_chunks(data, 65536), O.COracle(m).run(data, 65536, threads=8))
+
+
+def test_first_pass_live_early_stop(tmp_path):
+    """A general map with byte-pair keys ("qz" -> 'a', "ab" -> 256): its first pass reports whether
+    it made a token below 256.  Text without "qz": the byte pass is final (no u16 pass).  With "qzb"
+    sprinkled in: the u16 passes run and merge.  With "qz" only cut by chunk ends: final again.
+    The wrap-around merges file on text makes no token below 256 either."""
+    m = {(113, 122): 97, (97, 98): 256}
+    s = blt_amd.BpeStrategy(m)
+    assert _byte_mode(s) == {"mode": 1, "allmerge": False, "live": True}
+    cs = 1 << 16
+    text = synth.text(40 * cs + 99, seed=64).copy()
+    text[text == 113] = 120   # no 'q' at all
+    got = s.process_chunks(text, cs)
+    assert np.array_equal(got, O.COracle(m).run(text, cs, threads=8))
+    assert _u16_passes() == 0
+    t2 = text.copy()
+    for c in range(1, 40):
+        t2[c * cs - 1], t2[c * cs] = 113, 122   # "qz" across every chunk boundary: never merges
+    assert np.array_equal(s.process_chunks(t2, cs), O.COracle(m).run(t2, cs, threads=8))
+    assert _u16_passes() == 0
+    t3 = text.copy()
+    pos = np.random.default_rng(65).choice(t3.size - 3, 500, replace=False)
+    for q in pos:
+        t3[q:q + 3] = (113, 122, 98)
+    assert np.array_equal(s.process_chunks(t3, cs), O.COracle(m).run(t3, cs, threads=8))
+    assert _u16_passes() >= 1
+    path = str(tmp_path / "wrap.txt")
+    with open(path, "w") as f:
+        f.write(synth.wrap_merges_lines())
+    w = blt_amd.BpeStrategy.from_file(path)
+    assert _byte_mode(w) == {"mode": 1, "allmerge": True, "live": True}
+    wm = O.load_bpe_merges_from_path(path)
+    tw = synth.text((2 << 20) + 3, seed=66)
+    got, lens = w.process_chunks(tw, 1 << 20, return_chunk_lens=True)
+    exp, elens = O.COracle(wm).run(tw, 1 << 20, threads=8, return_lens=True)
+    assert np.array_equal(got, exp) and np.array_equal(lens, elens)
+    assert _u16_passes() == 0

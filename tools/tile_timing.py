@@ -30,10 +30,13 @@ def main():
     n = mib << 20
     if "--few" in sys.argv:   # two merges ("e ", "th"): ~0.97 tokens per byte, two-part emission
         merges = {(101, 32): 256, (116, 104): 257}
+    elif "--cfg2" in sys.argv:   # cfg2's 256 merges ranked from its text (seed 2)
+        merges = synth.merges_dict(synth.top_pair_merges(synth.text(100 << 20, seed=2), 256))
     else:
         merges = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
     s = blt_amd.BpeStrategy(merges)
-    data = synth.random_bytes(n, seed=5) if "--random" in sys.argv else synth.text(n, seed=3)   # cfg5 / cfg3
+    data = synth.random_bytes(n, seed=5) if "--random" in sys.argv else \
+        synth.text(n, seed=2 if "--cfg2" in sys.argv else 3)   # cfg5 / cfg2 / cfg3
     d_in = torch.from_numpy(data).cuda()
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
     wsb = s.workspace_size(n, CHUNK)
