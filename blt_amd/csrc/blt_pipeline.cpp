@@ -193,6 +193,7 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
         clock_gettime(CLOCK_MONOTONIC, &ts);
         return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
     };
+    double t_first = 0;
     for (size_t off = 0, k = 0; off < n && !rc; off += win, ++k) {
         const size_t len = std::min(win, n - off);
         Buf& out = buf[k & 1];
@@ -200,7 +201,10 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
         rc = st.window(in + off, len, cs, out);
         const double t1 = timing ? now() : 0;
         if (writer.joinable()) writer.join();   // window k-1 written: its buffer is free
-        if (timing) { t_tok += t1 - t0; t_wait += now() - t1; }
+        if (timing) {
+            if (k == 0) t_first = t1 - t0; else t_tok += t1 - t0;
+            t_wait += now() - t1;
+        }
         if (wrc) break;
         if (rc) break;
         writer = std::thread([&sink, &out, &wrc, &wmsg] {
@@ -213,8 +217,9 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
         if (writer.joinable()) writer.join();
         if (timing) {
             t_wait += now() - t1;
-            fprintf(stderr, "blt timing: %zu window(s) of %zu MiB: tokenise %.4f s, wait for writer %.4f s\n",
-                    (n + win - 1) / win, win >> 20, t_tok, t_wait);
+            fprintf(stderr, "blt timing: %zu window(s) of %zu MiB: first window %.4f s (device setup included), "
+                    "tokenise the rest %.4f s, wait for writer %.4f s\n", (n + win - 1) / win, win >> 20, t_first,
+                    t_tok, t_wait);
         }
     }
     if (rc) return rc;
@@ -343,6 +348,9 @@ int run(const blt_run_config* c) {
     const size_t cs = (size_t)c->chunk_size;
 
     // setup_io (io_handler.rs:55-62): the input is opened and mapped first
+    const bool timing = getenv("BLT_CLI_TIMING") != nullptr;
+    timespec ts0;
+    clock_gettime(CLOCK_MONOTONIC, &ts0);
     const uint8_t* map = nullptr;
     size_t n = 0;
     if (c->input_path) {
@@ -368,6 +376,12 @@ int run(const blt_run_config* c) {
         }
         ::close(fd);
     }
+    if (timing) {
+        timespec ts1;
+        clock_gettime(CLOCK_MONOTONIC, &ts1);
+        fprintf(stderr, "blt timing: input open + mmap (MAP_POPULATE) %.4f s\n",
+                (double)(ts1.tv_sec - ts0.tv_sec) + 1e-9 * (double)(ts1.tv_nsec - ts0.tv_nsec));
+    }
     struct Unmap {
         const uint8_t* p;
         size_t n;
@@ -383,6 +397,14 @@ int run(const blt_run_config* c) {
         sink.fd = ofd;
         sink.positioned = true;
     }
+    auto stamp = [&](const char* what) {
+        if (!timing) return;
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        fprintf(stderr, "blt timing: %s at %.4f s\n", what,
+                (double)(t.tv_sec - ts0.tv_sec) + 1e-9 * (double)(t.tv_nsec - ts0.tv_nsec));
+    };
+    stamp("output opened (truncated)");
     struct Close {
         int fd;
         ~Close() { if (fd > 2) ::close(fd); }
@@ -397,10 +419,12 @@ int run(const blt_run_config* c) {
         if (c->input_path) rc = run_mmap(st, map, n, cs, sink);
         else rc = run_stream(st, 0, cs, (size_t)c->threads, sink);
     }
+    stamp("chunks written");
     if (!rc && c->output_path) {
         closer.fd = -1;
         if (::close(ofd) != 0) rc = os_error(errno);
     }
+    stamp("output closed");
     return rc;
 }
 
