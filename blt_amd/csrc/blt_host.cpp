@@ -259,6 +259,9 @@ struct blt_bpe {
     // A general map whose keys are all byte pairs: its first pass reports whether it made a token
     // below 256 (the only key components), and is the fixpoint when it made none.
     bool live_first = false;
+    // General map: the longest merge chain (chain_depth; 0 = unbounded): the passes it needs are
+    // known up front, so they are enqueued without reading the device's pass count.
+    uint32_t chain_depth = 0;
     std::vector<uint16_t> self_ne, self_be;
     // General map (not single_pass): 2-choice cuckoo table of one-slot buckets for the u16 passes
     // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31
@@ -367,6 +370,47 @@ bool build_buckets(const std::unordered_map<uint32_t, uint16_t>& map, const std:
     return false;
 }
 
+// Longest merge chain of a general map: D(v) = 1 + max over keys (x, y) -> v of max(D(x), D(y)), and
+// D = 0 for a token no key produces.  A merge in u16 pass p involves a token pass p - 1 produced (a
+// pair of two older tokens was looked up in pass p - 1 and rejected), so it ends a chain of p + 1
+// merges: no pass after the max D-th merges anything.  0 when some value can be made from itself
+// (a cycle: the chain is unbounded, e.g. (97, 98) -> 97 on "abbb...").
+uint32_t chain_depth(const std::unordered_map<uint32_t, uint16_t>& map) {
+    std::unordered_map<uint32_t, std::vector<uint32_t>> prod;   // value -> keys that make it
+    for (const auto& kv : map) prod[kv.second].push_back(kv.first);
+    std::vector<uint32_t> depth(65536, 0);
+    std::vector<uint8_t> state(65536, 0);   // 0 unseen, 1 on the DFS stack, 2 done
+    struct Frame { uint32_t v; size_t i; uint32_t best; };
+    uint32_t maxd = 0;
+    for (const auto& pv : prod) {
+        if (state[pv.first]) continue;
+        std::vector<Frame> st{{pv.first, 0, 0}};
+        state[pv.first] = 1;
+        while (!st.empty()) {
+            Frame& f = st.back();
+            const std::vector<uint32_t>& ks = prod[f.v];
+            if (f.i < 2 * ks.size()) {
+                const uint32_t key = ks[f.i / 2];
+                const uint32_t c = (f.i & 1) ? (key & 0xFFFFu) : (key >> 16);
+                ++f.i;
+                if (!prod.count(c)) continue;                  // not a value: depth 0
+                if (state[c] == 1) return 0;                   // a cycle
+                if (state[c] == 2) { f.best = std::max(f.best, depth[c]); continue; }
+                state[c] = 1;
+                st.push_back({c, 0, 0});
+                continue;
+            }
+            depth[f.v] = f.best + 1;
+            state[f.v] = 2;
+            maxd = std::max(maxd, depth[f.v]);
+            const uint32_t d = depth[f.v];
+            st.pop_back();
+            if (!st.empty()) st.back().best = std::max(st.back().best, d);
+        }
+    }
+    return maxd;
+}
+
 int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>& vals, blt_bpe** out) {
     std::unique_ptr<blt_bpe> h(new (std::nothrow) blt_bpe());
     if (!h) return fail(BLT_E_NOMEM, "out of host memory");
@@ -387,6 +431,7 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
     }
     for (int t = 0; t < 65536 && h->single_pass; ++t)
         if (is_value[t] && is_comp[t]) h->single_pass = false;
+    if (!h->single_pass) h->chain_depth = chain_depth(map);
 
     // Dense byte-pair table for pass 1: value, or a sentinel no byte-pair key maps to.
     std::vector<uint8_t> used(65536, 0);
@@ -633,6 +678,21 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     return 0;
 }
 
+// A device error flagged during a general map's chain: the sticky message, with the control
+// block's flags and first-error record of the chain's u16 scan passes (their chunk-map kernel
+// resets only the ticket).
+int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t passes) {
+    if (!sticky_check(h)) return 0;
+    const std::string sticky_msg = t_err;
+    uint32_t ctl[16] = {0};
+    if (hipMemcpy(ctl, ws + L.ctl, sizeof ctl, hipMemcpyDeviceToHost) == hipSuccess && ctl_error(ctl))
+        return fail(BLT_E_IO, "%s; u16 passes 1..%llu: %s", sticky_msg.c_str(), (unsigned long long)passes, t_err.c_str());
+    return fail(BLT_E_IO, "%s", sticky_msg.c_str());
+}
+
+// Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
+constexpr uint32_t kMaxBoundedPasses = 64;
+
 int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
                   uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, hipStream_t s, uint64_t* out_tokens,
                   uint32_t flags = 0) {
@@ -692,6 +752,31 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     int cur = 0;
     uint64_t k = 1;   // u16 passes enqueued
     uint64_t rec[4] = {0, 0, 0, 0};
+    if (h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1) {
+        // a bounded chain (no value can be made from itself): u16 passes 1 .. depth - 1 are all a
+        // pass can need, enqueued without reading the device's pass count; passes after the one
+        // that marks the fixpoint return at once, and a last kernel picks the final pass's total
+        // and chunk offsets.  Only a caller asking for the token count waits (once).
+        const uint32_t k_last = h->chain_depth - 1;
+        for (; k <= k_last; ++k) {
+            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
+            const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
+            if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
+                                  false, &c, scan))
+                return rc;
+            cur ^= 1;
+        }
+        uint64_t* tot_final = tot + 3;   // the chain block's last word
+        HIP_TRY(blt::launch_chain_final(tot, done, off[1], d_chunk_off, L.nchunks, k_last, tot_final, s));
+        if (!out_tokens) return 0;
+        HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (int rc = chain_sticky(h, ws, L, k_last)) return rc;
+        const uint32_t kd = (uint32_t)rec[2];
+        t_last_u16_passes = kd ? (kd & ~blt::kDoneBytePass) : k_last;
+        *out_tokens = rec[3];
+        return 0;
+    }
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
@@ -703,17 +788,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         }
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (sticky_check(h)) {
-            // the control block holds the flags and first-error record of the chain's u16 scan
-            // passes (their chunk-map kernel resets only the ticket); report them with the sticky
-            // message
-            const std::string sticky_msg = t_err;
-            uint32_t ctl[16] = {0};
-            if (hipMemcpy(ctl, ws + L.ctl, sizeof ctl, hipMemcpyDeviceToHost) == hipSuccess && ctl_error(ctl))
-                return fail(BLT_E_IO, "%s; u16 passes 1..%llu: %s", sticky_msg.c_str(), (unsigned long long)(k - 1),
-                            t_err.c_str());
-            return fail(BLT_E_IO, "%s", sticky_msg.c_str());
-        }
+        if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
         if ((uint32_t)rec[2]) break;
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
@@ -1272,6 +1347,9 @@ int blt_debug_byte_mode(const blt_bpe* h) {
     if (!h) return -1;
     return (h->byte_mode & 0xFF) | (h->allmerge ? 0x100 : 0) | (h->live_first ? 0x200 : 0);
 }
+
+// Not in the public header: a general map's longest merge chain (0: single-pass, or unbounded).
+uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0; }
 
 // Not in the public header: a test hook that makes blt_bpe_process_chunks run n_gpus device
 // contexts even where several share a device (on a one-GPU box: every context's producer and drain

@@ -82,6 +82,10 @@ constexpr uint32_t kDoneBytePass = 0x80000000u;
 // at least kTokRange tokens.
 hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
+// The end of a general map's chain enqueued up to its known depth: the final pass (the done word's,
+// else k_last) gives *tot_final and, when it wrote off1, the caller's chunk offsets.
+hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const uint64_t* off1, uint64_t* chunk_off,
+                              uint64_t nchunks, uint32_t k_last, uint64_t* tot_final, hipStream_t s);
 // Test hook: runs the kernels' error path once (ctl nullable, sticky the handle's error word).
 hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s);
 

@@ -2190,6 +2190,20 @@ __global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __rest
     }
 }
 
+// End of a general map's chain enqueued without reading its pass count (the map's chain depth
+// bounds the passes): the final pass is the one the done word names, else the last enqueued
+// (k_last); its total goes to tot_final, and its chunk offsets to the caller's array when that
+// pass wrote the other one (pass k writes offsets [k & 1]).
+__global__ __launch_bounds__(256) void chain_final_kernel(const uint64_t* tot, const uint32_t* done, const uint64_t* off1,
+                                                          uint64_t* chunk_off, uint64_t nchunks, uint32_t k_last,
+                                                          uint64_t* tot_final) {
+    const uint32_t d = __hip_atomic_load(const_cast<uint32_t*>(done), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t k = d ? (d & ~kDoneBytePass) : k_last;
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i == 0) *tot_final = tot[k & 1u];
+    if (chunk_off && (k & 1u) && i <= nchunks) chunk_off[i] = off1[i];
+}
+
 __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
     if (threadIdx.x == 0) flag_error(ctl, sticky, 1u);
 }
@@ -2309,6 +2323,14 @@ hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipS
     if (blocks < 1) blocks = 1;
     if (blocks > BLT_BASIC_BLOCKS) blocks = BLT_BASIC_BLOCKS;
     hipLaunchKernelGGL(basic_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const uint64_t* off1, uint64_t* chunk_off,
+                              uint64_t nchunks, uint32_t k_last, uint64_t* tot_final, hipStream_t s) {
+    const uint64_t blocks = chunk_off ? (nchunks + 1 + 255) / 256 : 1;
+    hipLaunchKernelGGL(chain_final_kernel, dim3((unsigned)blocks), dim3(256), 0, s, tot, done, off1, chunk_off, nchunks,
+                       k_last, tot_final);
     return hipGetLastError();
 }
 

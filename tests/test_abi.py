@@ -188,3 +188,26 @@ def test_tokenising_without_gpu_fails_loudly():
     with pytest.raises(blt_amd.BltError) as ei:
         s.process_chunk(b"abab")
     assert ei.value.kind == "NoDevice"
+
+
+def test_chain_depth_of_general_maps(tmp_path):
+    """The longest merge chain bounds the passes a general map needs (host-only: handle creation)."""
+    from blt_amd import synth
+    L = _lib.lib()
+
+    def depth(m):
+        s = blt_amd.BpeStrategy(m)
+        d = L.blt_debug_chain_depth(s.handle)
+        s.close()
+        return d
+    assert depth({(97, 98): 256}) == 0                      # single-pass
+    assert depth(synth.CHAINED_TEXT_MAP) == 2
+    assert depth(synth.doubling_chain(24)) == 24
+    assert depth({(97, 98): 65, (65, 99): 300, (300, 300): 301}) == 3
+    assert depth(synth.SELF_VALUED_MAP) == 0                # "e " -> e: a value made from itself
+    assert depth({(97, 98): 97}) == 0
+    assert depth({(97, 98): 120, (120, 99): 97}) == 0      # a two-step cycle
+    path = tmp_path / "wrap.txt"
+    path.write_text(synth.wrap_merges_lines())
+    s = blt_amd.BpeStrategy.from_file(str(path))
+    assert L.blt_debug_chain_depth(s.handle) == 0           # (255, 255) -> 255

@@ -790,3 +790,44 @@ def test_first_pass_live_early_stop(tmp_path):
     exp, elens = O.COracle(wm).run(tw, 1 << 20, threads=8, return_lens=True)
     assert np.array_equal(got, exp) and np.array_equal(lens, elens)
     assert _u16_passes() == 0
+
+
+@pytest.mark.parametrize("name", ["chained", "depth3", "depth4", "cyclic"])
+def test_general_map_async_enqueue(name):
+    """A general map whose merge chains are bounded enqueues all its passes without reading the
+    device's pass count (blt_bpe_encode_device returns at once when no token count is asked for);
+    a final kernel moves the last pass's chunk offsets into the caller's array (odd and even final
+    passes).  A cyclic map runs host-checked batches.  Output, total and chunk offsets against the
+    oracle, the async form against the sync one."""
+    import torch
+    maps = {"chained": CHAINED_TEXT_MAP, "depth3": {(97, 97): 256, (256, 256): 257, (257, 257): 258},
+            "depth4": {(97, 97): 256, (256, 256): 257, (257, 257): 258, (258, 258): 259},
+            "cyclic": {(101, 32): 101, (116, 104): 256}}
+    m = maps[name]
+    s = blt_amd.BpeStrategy(m)
+    if name == "cyclic":
+        assert blt_amd._lib.lib().blt_debug_chain_depth(s.handle) == 0
+    text = synth.text((2 << 20) + 33, seed=71).copy()
+    text[::7] = 97   # runs of 'a' long enough for the doubling chains here and there
+    text[1::7] = 97
+    cs = 65536 + 3
+    n = text.size
+    nchunks = (n + cs - 1) // cs
+    d_in = torch.from_numpy(text).cuda()
+    exp, elens = O.COracle(m).run(text, cs, threads=8, return_lens=True)
+    for sync in (True, False):
+        d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+        d_off = torch.full((nchunks + 1,), -1, dtype=torch.int64, device="cuda")
+        ws_b = s.workspace_size(n, cs)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), ws_b, stream,
+                              d_off.data_ptr(), sync=sync)
+        torch.cuda.synchronize()
+        offs = d_off.cpu().numpy()
+        if sync:
+            assert 2 * tok == exp.size
+        tok = int(offs[-1])
+        assert 2 * tok == exp.size, (name, sync)
+        assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp), (name, sync)
+        assert np.array_equal(np.diff(offs) * 2, elens), (name, sync)
