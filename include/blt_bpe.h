@@ -161,10 +161,11 @@ size_t blt_bpe_workspace_size(const blt_bpe *h, uint64_t n, uint64_t chunk_size)
  * 16-byte aligned; receives the stitched big-endian token stream.  d_chunk_off (nullable):
  * nchunks + 1 u64, the output token index where each chunk starts, [nchunks] = total tokens.
  * d_workspace: blt_bpe_workspace_size() bytes.  out_tokens (nullable): if given, the call
- * waits for the stream and returns the number of output tokens; if NULL and the map is
- * single-pass, the call only enqueues work (no host synchronisation).  A general map (several
- * passes) waits for the stream after its first u16 pass and then after every 4, to read
- * whether the chain has reached its fixpoint. */
+ * waits for the stream and returns the number of output tokens; if NULL, the call only enqueues
+ * work (no host synchronisation) for every single-pass map and for every general map whose merge
+ * chains are bounded (no value can be made from itself: its passes are known up front).  A
+ * general map with a cycle (e.g. (97, 98) -> 97) waits for the stream after its first u16 pass
+ * and then after every 4, to read whether the chain has reached its fixpoint. */
 int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
                           uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
                           void *stream, uint64_t *out_tokens);
