@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip configs / end_to_end / per_chunk_path / cli")
     ap.add_argument("--only-configs", default="", help="comma list: run only these `configs` rows")
+    ap.add_argument("--events-in-timed-loop", action="store_true",
+                    help="record the kernel's HIP events inside the timed loop (default: a second loop)")
     ap.add_argument("--workload", default="", choices=["", "cfg2", "cfg3", "cfg4", "cfg5"],
                     help="default: cfg3 at N = 1, cfg4 at N > 1")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("BLT_CPU_THREADS", "0")),
@@ -415,17 +417,25 @@ def main():
     strategy.check_workspace(ws.data_ptr(), sp)
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    timed_events = args.events_in_timed_loop
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(*evs[i])
+        step(*(evs[i] if timed_events else (None, None)))
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     strategy.check_workspace(ws.data_ptr(), sp)
+    if not timed_events:
+        # the kernel's own duration: the same steps again with HIP events around each launch (event
+        # records between launches are instrumentation, kept out of the timed loop of `value`)
+        for i in range(args.steps):
+            step(*evs[i])
+        torch.cuda.synchronize()
+        strategy.check_workspace(ws.data_ptr(), sp)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tokens = int(d_off[-1].item())
 
