@@ -38,6 +38,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stddef.h>
+
 #include <atomic>
 #include <mutex>
 #include <unordered_map>
@@ -137,10 +139,30 @@ __device__ __forceinline__ void flag_error(uint32_t* ctl, uint32_t* sticky, uint
     if (sticky) __hip_atomic_store(sticky, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A PassParams field read again from the kernel-argument segment where it is used (one scalar
+// load; every kernel here takes the PassParams as its only argument), for fields the error,
+// last-tile and record paths need: kept live across the persistent loops they would cost SGPRs the
+// byte pass spills to VGPR lanes (34 spills, ~240 v_readlane in its body before this).
+template <typename T>
+__device__ __forceinline__ T karg_reload(size_t off) {
+    typedef const volatile T __attribute__((address_space(4))) cvT;
+    return *(cvT*)((const char __attribute__((address_space(4)))*)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+#define KARG(field) karg_reload<decltype(PassParams::field)>(offsetof(PassParams, field))
+// Per-tile debug records (tests/debug_replay.py, the timing tools) only in builds that ask for them.
+#ifndef BLT_DEBUG_RECORD
+#define BLT_DEBUG_RECORD 0
+#endif
+#ifdef BLT_TIMING
+constexpr bool kDebugRecord = true;
+#else
+constexpr bool kDebugRecord = BLT_DEBUG_RECORD != 0;
+#endif
+
 // First failure wins: ctl[2] = T + 1, ctl[3] = sub-tile, ctl[4..5] = O, ctl[6..7] = value, ctl[8] = C.
 __device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint32_t j, uint64_t O, uint64_t v,
                              uint32_t C) {
-    flag_error(p.ctl, p.sticky, bit);
+    flag_error(p.ctl, KARG(sticky), bit);
     if (atomicCAS(p.ctl + 2, 0u, T + 1u) == 0u) {
         p.ctl[3] = j;
         p.ctl[4] = (uint32_t)O; p.ctl[5] = (uint32_t)(O >> 32);
@@ -179,7 +201,7 @@ __device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t&
         uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
         if ((ready & need) != need) {
             if (++spins > kSpinLimit) {   // flagged; the tile writes nothing (C = 2)
-                if (lane == 0) flag_error(p.ctl, p.sticky, 1u);
+                if (lane == 0) flag_error(p.ctl, KARG(sticky), 1u);
                 C = 2u; O = 0ull;
                 return;
             }
@@ -761,11 +783,12 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
         t.k0 = (uint64_t)q + (r ? 1u : 0u);
         return t;
     }
-    uint64_t q = __umul64hi(tile0, p.cs_magic);
-    uint64_t r = tile0 - q * p.cs;
-    if (r >= p.cs) { q += 1; r -= p.cs; }
-    if (r >= p.cs) { q += 1; r -= p.cs; }
-    const uint64_t d = r ? p.cs - r : 0;
+    const uint64_t cs = KARG(cs);   // (this path only: chunk sizes that are no whole number of tiles)
+    uint64_t q = __umul64hi(tile0, KARG(cs_magic));
+    uint64_t r = tile0 - q * cs;
+    if (r >= cs) { q += 1; r -= cs; }
+    if (r >= cs) { q += 1; r -= cs; }
+    const uint64_t d = r ? cs - r : 0;
     t.bge = (uint32_t)(d > 0x10000ull ? 0x10000ull : d);
     t.k0 = q + (r ? 1u : 0u);
     return t;
@@ -1063,7 +1086,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
         }
         if (!ready) {
             if (++spins > kLbSpinLimit) {   // flagged; the tile writes nothing (C = 2)
-                if (lane == 0) flag_error(p.ctl, p.sticky, 1u);
+                if (lane == 0) flag_error(p.ctl, KARG(sticky), 1u);
                 C = 2u; O = 0ull;
                 return;
             }
@@ -1304,11 +1327,12 @@ struct SparseRange {
 // boundary at or below byte 2 O, so every offset below is 32-bit.
 __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, const TInfo& ti, uint32_t cs32,
                                           uint32_t wave, int lane, const TileState& st, const uint32_t (*gin)[4],
-                                          uint32_t C, uint64_t O, uint8_t* stg) {
-    uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
+                                          uint32_t C, uint64_t O, uint8_t* stg, bool has_coff) {
+    uint8_t* out = reinterpret_cast<uint8_t*>(KARG(out));   // (reloaded per tile: fewer live SGPRs)
+    const uint64_t out_cap = KARG(out_cap);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
-    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, p.out_cap > obase ? p.out_cap - obase : 0);
+    const __amdgpu_buffer_rsrc_t ro = rsrc_at(out + obase, out_cap > obase ? out_cap - obase : 0);
     const uint32_t stg_lds = lds_addr(stg);
     uint32_t cnext = ti.bge;   // first chunk start >= the wave range's first position
     uint64_t kc = ti.k0;       // its chunk index
@@ -1323,12 +1347,12 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t gb = orel + 2u * goff;              // output byte of the wave range, from obase
         // chunk start inside this wave range (cs >= 4096 > kWavePos: at most one)
         while (cnext < wrel) { cnext += cs32; ++kc; }   // uniform; kSubPos / 4096 steps at most
-        const bool cstart = p.chunk_off && cnext < ti.rn && cnext - wrel < kWavePos;
+        const bool cstart = has_coff && cnext < ti.rn && cnext - wrel < kWavePos;
         sparse[j] = __ballot(st.mv[j] != 0xFFFFFFFFu) != 0;
         if (!sparse[j]) {
             // dense: every pair merges, no buffer end, so no chunk end: a chunk can only start at
             // the range's first position
-            if (cstart && lane == 0) p.chunk_off[kc] = O + goff;
+            if (cstart && lane == 0) KARG(chunk_off)[kc] = O + goff;
             emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
             continue;
         }
@@ -1342,7 +1366,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
         if (cstart) {
             const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
-            if (e < 16u) p.chunk_off[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+            if (e < 16u) KARG(chunk_off)[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
         sr[j].L = L;
         sr[j].lane_off = lane_off;
@@ -1380,7 +1404,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
 // wait for them right here.
 __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint32_t wave, int lane,
                                           uint32_t (&x)[kS][4], uint32_t (&nxt)[kS]) {
-    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(KARG(in));   // (reloaded per tile)
     const uint64_t tile0 = (uint64_t)Tn * kTilePosBytes;
     const uint64_t left = p.n > tile0 ? p.n - tile0 : 0;
     const __amdgpu_buffer_rsrc_t r = rsrc_at(in + tile0, left);
@@ -1446,7 +1470,7 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
     uint32_t spins = 0;
     while (lds_acquire(f) < v) {
         if (++spins > kWaitLimit) {
-            if ((threadIdx.x & 63) == 0) flag_error(p.ctl, p.sticky, 8u);
+            if ((threadIdx.x & 63) == 0) flag_error(p.ctl, KARG(sticky), 8u);
             break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -1490,6 +1514,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t ntiles = p.ntiles;
     const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
+    const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
@@ -1606,13 +1631,14 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
                 lds_release(&s_lbdone, it + 1u);
                 const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
                 if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
-                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
+                if (2ull * fin > KARG(out_cap)) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
-                    *p.total = fin;
-                    if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
-                    if (kLive && p.done && C <= 1u && (fin == n || !live)) *p.done = kDoneBytePass;
+                    *KARG(total) = fin;
+                    if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
+                    if (kLive && C <= 1u && (fin == n || !live))
+                        if (uint32_t* dn = KARG(done)) *dn = kDoneBytePass;
                 }
-                if (p.debug) {
+                if (kDebugRecord && p.debug) {
                     uint64_t* d = p.debug + 4ull * Tp;
                     d[0] = O;
                     d[1] = ((uint64_t)C << 32) | how;
@@ -1635,7 +1661,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
             const uint32_t Cp = uni(s_C[pslot]);
             if (Cp <= 1u)   // C = 2: a failed tile (flagged), no output
-                emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], Cp, uni64(s_O[pslot]), s_stage[wave]);
+                emit_tile(p, Tp, tip, cs32, wave, lane, sp, s_gin[pslot], Cp, uni64(s_O[pslot]), s_stage[wave], has_coff);
             __builtin_amdgcn_s_setprio(0);
         }
         if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
@@ -1757,7 +1783,7 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
         w |= ((cs[e] - 1 - lo) << 12) | kCmEnd;
         bad |= e + 1 < nc && cs[e + 1] <= hi;
     }
-    if (bad) flag_error(p.ctl, p.sticky, 16u);   // chunks shorter than a wave range: host bug
+    if (bad) flag_error(p.ctl, KARG(sticky), 16u);   // chunks shorter than a wave range: host bug
     p.cmap[r] = w;
 }
 
@@ -1897,7 +1923,7 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
 // rem: tokens from the range start to the buffer end; wtok: the range's first input token.
 __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uint32_t rem, uint32_t cwl, uint32_t cwh,
                                          int lane, int j, const TileStateT<kSt>& st, const uint32_t* gin,
-                                         uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave) {
+                                         uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave, bool has_coff) {
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
@@ -1905,10 +1931,10 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t cg = uni(gin[C]);
     const uint32_t goff = uni(gin[2 + C]);   // tokens before this wave range in the tile
     const uint32_t gb = orel + 2u * goff;    // output byte of the wave range, from obase
-    const bool cstart = p.chunk_off && (cwl & kCmStart) != 0u;
+    const bool cstart = has_coff && (cwl & kCmStart) != 0u;
     if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
         // dense: every pair merges, so the only possible chunk start is the range's first token
-        if (cstart && lane == 0) p.chunk_off[cwh] = O + goff;
+        if (cstart && lane == 0) KARG(chunk_off)[cwh] = O + goff;
         emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
     }
@@ -1922,7 +1948,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
     if (cstart) {
         const uint32_t e = (cwl & 0x7FFu) - 16u * (uint32_t)lane;
-        if (e < 16u) p.chunk_off[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+        if (e < 16u) KARG(chunk_off)[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
@@ -1955,6 +1981,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     const int lane = tid & 63;
     const uint32_t wave = uni((uint32_t)tid >> 6);
     const uint64_t n = uni64(token_count(p));
+    const bool has_coff = p.chunk_off != nullptr;
     const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
     // tokens from sub-tile j's wave range start of tile T to the buffer end (clamped)
     auto rem_of = [&](uint32_t T, int j) {
@@ -2063,14 +2090,14 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
                 if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
                 if (Tp == ntiles - 1) {
-                    *p.total = fin;
-                    if (p.chunk_off) p.chunk_off[p.nchunks] = fin;
+                    *KARG(total) = fin;
+                    if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
                     // The fixpoint: this pass merged nothing, or none of its merges made a key
                     // component, so the next pass merges nothing (a pair of two tokens this pass
                     // left alone was looked up here and rejected; a new token is in no key).
                     if (p.done && C <= 1u && (fin == n || !live)) *p.done = p.pass_id;
                 }
-                if (p.debug) {
+                if (kDebugRecord && p.debug) {
                     uint64_t* d = p.debug + 4ull * Tp;
                     d[0] = O;
                     d[1] = ((uint64_t)C << 32) | how;
@@ -2092,7 +2119,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 for (int j = 0; j < kSt; ++j) {
                     const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
                     emit_tok(p, wtok, rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
-                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave);
+                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff);
                 }
             }
             __builtin_amdgcn_s_setprio(0);
