@@ -1,5 +1,9 @@
 """Debug aid: replays one stress-test input on the GPU and compares every tile's look-back status
-word with a sequential scan.  python tests/debug_replay.py <stress-iteration> [repeats]"""
+word with a sequential scan.  python tests/debug_replay.py <stress-iteration> [repeats]
+
+The per-tile records exist only in a record build of the kernels:
+    tools/build_variant.sh record -DBLT_DEBUG_RECORD=1
+    BLT_LIB_PATH=build/exp/libblt_bpe_record.so python tests/debug_replay.py N"""
 import os
 import random
 import sys
