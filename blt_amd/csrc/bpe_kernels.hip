@@ -372,6 +372,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
             p.n = __hip_atomic_load(const_cast<uint64_t*>(p.n_dev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             p.ntiles = (uint32_t)((p.n + kTileT - 1) / kTileT);
         }
+        // the grid was sized for the input's bound; workgroups past the tiles there are leave
+        // before copying the table (the ones below claim every ticket)
+        if (blockIdx.x >= p.ntiles) return;
     }
     const InT* in = reinterpret_cast<const InT*>(p.in);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
@@ -1983,6 +1986,9 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     const uint64_t n = uni64(token_count(p));
     const bool has_coff = p.chunk_off != nullptr;
     const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
+    // the grid was sized for the token bound; workgroups past the tiles the previous pass left leave
+    // before copying the table (the ones below claim every ticket)
+    if (blockIdx.x >= ntiles) return;
     // tokens from sub-tile j's wave range start of tile T to the buffer end (clamped)
     auto rem_of = [&](uint32_t T, int j) {
         const uint64_t w0 = (uint64_t)T * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
