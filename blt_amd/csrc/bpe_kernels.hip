@@ -696,15 +696,6 @@ constexpr int kGroups = kS * kWaves;
 // or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
 // in two parts of 32 lanes (at most 512 tokens each).
 constexpr int kStageWave = 1536 * (16 / kWaves);    // the LDS the table leaves, shared by the waves
-// Timing experiment only (BLT_EXP_HALFTAB, wrong output for bytes >= 128): the table's first 128
-// rows and input bytes masked to 7 bits, so two workgroups fit one CU's LDS.
-#ifdef BLT_EXP_HALFTAB
-constexpr uint32_t kTabLds = 128 * kSelfRow;
-constexpr int kStageWaveX = 1280;
-#else
-constexpr uint32_t kTabLds = kSelfEntries;
-constexpr int kStageWaveX = kStageWave;
-#endif
 // Look-back windows of 64 status words per round trip.  (Measured: 2 or 4 windows cost more
 // through register spills than the extra round trips they save.)
 constexpr int kLbWin = 1;
@@ -1236,7 +1227,7 @@ __device__ __forceinline__ void stage_b16_pad(const uint32_t (&v)[8], uint32_t L
 
 // Copy-out of one stage part: whole 16-byte blocks (at most kCopyBlk per lane) and the head and
 // tail fragments (u16 each, lanes 0..7 and 8..15).
-constexpr int kCopyBlk = (kStageWaveX + 1023) / 1024;
+constexpr int kCopyBlk = (kStageWave + 1023) / 1024;
 // The u16 scan kernel has no 128 KiB table in LDS: its per-wave stage holds a whole wave range's
 // tokens (a 2-byte aligned start and up to 1024 tokens), so every range goes out in one part.
 // Few of its positions merge, so a lane's tokens fill ~32 bytes and the 32 lanes of a store write
@@ -1275,8 +1266,8 @@ __device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c,
     if (BLT_OOB_COPY) {   // unconditional LDS reads inside the workgroup's LDS (junk where not stored)
 #pragma unroll
         for (int q = 0; q < NB; ++q)
-            d.vb[q] = *reinterpret_cast<const u32x4*>(sp + min(hend + 16u * lane + 1024u * q, (uint32_t)kStageWaveX - 16u));
-        d.vf = reinterpret_cast<const uint16_t*>(sp)[min(of >> 1, (uint32_t)kStageWaveX / 2u - 1u)];
+            d.vb[q] = *reinterpret_cast<const u32x4*>(sp + min(hend + 16u * lane + 1024u * q, (uint32_t)kStageWave - 16u));
+        d.vf = reinterpret_cast<const uint16_t*>(sp)[min(of >> 1, (uint32_t)kStageWave / 2u - 1u)];
         return;
     }
 #pragma unroll
@@ -1385,7 +1376,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         sr[j].gb = gb;
         sr[j].wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     }
-    auto fits = [&](int j) { return (sr[j].gb & 15u) + 2u * sr[j].wcnt <= (uint32_t)kStageWaveX; };
+    auto fits = [&](int j) { return (sr[j].gb & 15u) + 2u * sr[j].wcnt <= (uint32_t)kStageWave; };
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         if (!sparse[j]) continue;
@@ -1427,16 +1418,10 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, BLT_LDPOL);
         x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
-#ifdef BLT_EXP_HALFTAB
-        x[j][0] &= 0x7F7F7F7Fu; x[j][1] &= 0x7F7F7F7Fu; x[j][2] &= 0x7F7F7F7Fu; x[j][3] &= 0x7F7F7F7Fu;
-#endif
         // the byte after the range, as its whole (4-aligned) dword: a u8 load would be masked
         // right here, which makes the compiler wait for it.  The range check covers voffset
         // only, never soffset: offsets go in voffset.
         nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(wrel + kWavePos), 0, 0);
-#ifdef BLT_EXP_HALFTAB
-        nxt[j] &= 0x7F7F7F7Fu;
-#endif
     }
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
@@ -1510,14 +1495,9 @@ __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, 
 // nothing (a pair this pass left alone was looked up and rejected; a token >= 256 is in no key),
 // so the u16 passes the host enqueued behind it return at once.
 template <bool kBE, int kMode, bool kLive>
-#ifdef BLT_EXP_WPE
-#define BLT_BYTES_ATTR __attribute__((amdgpu_waves_per_eu(BLT_EXP_WPE)))
-#else
-#define BLT_BYTES_ATTR
-#endif
-__global__ __launch_bounds__(kThreads) BLT_BYTES_ATTR void scan_bytes_kernel(PassParams p) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_tab[kTabLds];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWaveX];
+__global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_tab[kSelfEntries];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves][kStageWave];
     __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroups][4];   // wave functions (phase 1)
     __shared__ uint32_t s_gin[kRing][kGroups][4];   // group carry-in |H=0,1, offset |H=0,1
     __shared__ uint32_t s_tfn[kRing][4];            // tile co0, co1, tot0, tot1
@@ -1556,7 +1536,7 @@ __global__ __launch_bounds__(kThreads) BLT_BYTES_ATTR void scan_bytes_kernel(Pas
         // LDS-DMA, every load in flight at once (one wave-instruction fills 1 KiB of LDS).  (A
         // rolled copy loop waits for each load: one L2/MALL round trip each, ~0.7 us when all 256
         // workgroups copy at once, 6.9 us in all.)
-        constexpr int kUnits = (int)(kTabLds * 2 / 16);
+        constexpr int kUnits = (int)(kSelfEntries * 2 / 16);
         constexpr int kPer = (kUnits + kThreads - 1) / kThreads;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
