@@ -85,16 +85,18 @@ def main():
         result["hbm_bytes_per_launch"] = int((2.0 * pd["FETCH_SIZE"] + pd["WRITE_SIZE"]) * 1024)
         result["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 FETCH_SIZE counts half of wide reads"
         # what bench.py reports as roofline.traffic for the same workload
-        n, wl = GIB, "cfg3"
+        sys.path.insert(0, ROOT)
+        import bench
+        per_gpu, total, wl = GIB, 0, "cfg3"
         for i, x in enumerate(bench_args):
             if x == "--bytes-per-gpu":
-                n = int(bench_args[i + 1])
+                per_gpu = int(bench_args[i + 1])
             if x == "--workload":
                 wl = bench_args[i + 1]
             if x == "--total-bytes":
-                n = int(bench_args[i + 1])
-        sys.path.insert(0, ROOT)
-        import bench
+                total = int(bench_args[i + 1])
+        # the bytes one launch processes at N = 1 (bench.workload's shapes)
+        n = 100 << 20 if wl == "cfg2" else per_gpu if wl == "cfg3" else (total or bench.STRONG_TOTAL[wl])
         with open(os.path.join(a.outdir, "traffic.json"), "w") as f:
             json.dump({"workload": wl, "bytes_per_gpu": n, "chunk_size": CHUNK, "kernel": a.kernel,
                        "kernel_source_sha256": bench.kernel_source_sha(),
