@@ -199,8 +199,10 @@ def O_load(path):
 
 
 def general_map_rate(blt_amd, synth, O, threads, name="multi", reps=10):
-    """A general map, device-resident; the timed region is the whole encode_device call (byte
-    pass, u16 passes, the host's read of the pass count)."""
+    """A general map, device-resident.  `ms`: the whole asynchronous encode_device call (every
+    pass enqueued, HIP events around it); `sync_ms`: the call that returns the token count (host
+    wall clock), where eligible maps run passes 1 and 2 fused (`sync_path`); the output checked is
+    the synchronous call's."""
     import torch
     host, make, merges, desc = general_workload(synth, name)
     n = host.size
@@ -222,6 +224,14 @@ def general_map_rate(blt_amd, synth, O, threads, name="multi", reps=10):
         ts.append(e0.elapsed_time(e1))
     ms = float(np.median(ts))
     passes = int(blt_amd._lib.lib().blt_debug_last_u16_passes())
+    # the same call asking for the token count (the host waits for it): eligible maps fuse passes 1
+    # and 2 into one kernel there (blt_debug_last_fused: 1 fused, 2 fell back, 0 two kernels)
+    tw = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        s.encode_device(d_in.data_ptr(), n, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
+        tw.append(time.perf_counter() - t0)
+    sync_path = {0: "two kernels", 1: "fused passes 1+2", 2: "fused, fell back"}[int(blt_amd._lib.lib().blt_debug_last_fused())]
     got = d_out[:2 * tok].cpu().numpy()
     exp = O.COracle(merges).run(host, CHUNK, threads=threads)
     algo = n + 2 * tok
@@ -229,6 +239,7 @@ def general_map_rate(blt_amd, synth, O, threads, name="multi", reps=10):
     return {"workload": desc, "bytes": n, "ms": round(ms, 4), "u16_passes": passes,
             "input_GBps": round(n / ms / 1e6, 1), "achieved_GBps": round(algo / ms / 1e6, 1),
             "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4), "tokens_per_byte": round(tok / n, 4),
+            "sync_ms": round(1000 * float(np.median(tw)), 4), "sync_path": sync_path,
             "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
 
 

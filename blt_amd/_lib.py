@@ -93,6 +93,8 @@ _DEBUG_SIGNATURES = {
     "blt_debug_set_tile_record": (None, [_vp]),
     "blt_debug_last_u16_passes": (ctypes.c_uint32, []),
     "blt_debug_set_shared_contexts": (None, [ctypes.c_int]),
+    "blt_debug_set_fused": (None, [ctypes.c_int]),
+    "blt_debug_last_fused": (ctypes.c_uint32, []),
     "blt_debug_byte_mode": (ctypes.c_int, [_vp]),
     "blt_debug_chain_depth": (ctypes.c_uint32, [_vp]),
     "blt_debug_available_cpus": (ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]),

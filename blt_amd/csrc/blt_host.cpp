@@ -557,9 +557,16 @@ int sticky_check(const blt_bpe* h) {
 uint64_t* g_debug_tiles = nullptr;
 // Test hook: n_gpus contexts even where they share a device (blt_debug_set_shared_contexts).
 std::atomic<int> g_shared_contexts{0};
+// Passes 1 and 2 of eligible general maps in one kernel (blt_debug_set_fused(0): the two-kernel
+// chain, for A/B runs and tests).
+std::atomic<int> g_fused{1};
+constexpr uint32_t kEncodeNoFused = 1u << 31;   // internal encode_device flag: the two-kernel chain
 // Test hook: u16 passes the calling thread's last synchronous general-map encode ran before the
 // chain stopped (blt_debug_last_u16_passes).
 thread_local uint32_t t_last_u16_passes = 0;
+// Test hook: how the calling thread's last synchronous general-map encode ran passes 1 and 2:
+// 0 two kernels, 1 fused, 2 fused and fell back (blt_debug_last_fused).
+thread_local uint32_t t_last_fused = 0;
 
 // ---- workspace layout -------------------------------------------------------------------
 inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -678,6 +685,41 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     return 0;
 }
 
+// Passes 1 and 2 of a general map in one launch (blt::launch_scan_fused): bytes d_in to the second
+// pass's tokens in d_out, its total, chunk offsets and done word as u16 pass 1's.
+int run_fused(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
+              const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out, uint64_t* chunk_off, uint64_t* total,
+              uint32_t* done, uint32_t* fused_fail) {
+    const uint64_t ntiles = (n + blt::kTilePosTok - 1) / blt::kTilePosTok;
+    if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
+    blt::PassParams p{};
+    p.in = d_in;
+    p.n = n;
+    p.cs = cs;
+    p.nchunks = L.nchunks;
+    p.out = d_out;
+    p.out_cap = 2 * n;
+    p.chunk_off = chunk_off;
+    p.status = reinterpret_cast<uint64_t*>(ws + L.status);
+    p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
+    p.total = total;
+    p.done = done;
+    p.pass_id = 1;
+    p.ntiles = (uint32_t)ntiles;
+    p.hbuckets = t->hbuckets;
+    p.hmul1 = h->hmul1;
+    p.hmul2 = h->hmul2;
+    p.hshift = h->hshift;
+    p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
+    p.hone = h->hone ? 1u : 0u;
+    p.cs_magic = ~0ull / cs;
+    p.debug = g_debug_tiles;
+    p.sticky = h->sticky.load(std::memory_order_acquire);
+    p.fused_fail = fused_fail;
+    HIP_TRY(blt::launch_scan_fused(p, dev, s));
+    return 0;
+}
+
 // A device error flagged during a general map's chain: the sticky message, with the control
 // block's flags and first-error record of the chain's u16 scan passes (their chunk-map kernel
 // resets only the ticket).
@@ -744,15 +786,35 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // pass 1's control block and status words and the chain's totals are contiguous: one memset
     // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
     HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + 32, s));
-    {   // pass 1 (pass id 0): with byte-pair keys it marks itself final when it made no key component
+    const bool bounded = h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1;
+    // Passes 1 and 2 in one kernel (run_fused) when the bucket table fits in LDS, chunks hold whole
+    // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
+    // keep the byte pass, which can); its halo fallback is read where the host reads the chain's
+    // totals anyway, so an async bounded chain keeps the two-kernel path.
+    const bool fused = !(flags & kEncodeNoFused) && g_fused.load(std::memory_order_relaxed) && !h->live_first &&
+                       h->hwords.size() * sizeof(uint32_t) <= blt::kHashLdsMax && cs >= blt::kMinChunkBytes &&
+                       (!bounded || out_tokens != nullptr);
+    uint32_t* fused_fail = reinterpret_cast<uint32_t*>(ws + L.total + 20);   // beside the done word
+    int cur = 0;
+    uint64_t k = 1;   // u16 passes enqueued
+    if (fused) {
+        if (int rc = run_fused(h, t, dev, s, ws, L, d_in, n, cs, d_out, off[1], tot + 1, done, fused_fail)) return rc;
+        cur = 1;
+        k = 2;
+    } else {   // pass 1 (pass id 0): with byte-pair keys it marks itself final when it made no key component
         const Chain c0{nullptr, tot, done, 0};
         if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0], true, &c0))
             return rc;
     }
-    int cur = 0;
-    uint64_t k = 1;   // u16 passes enqueued
+    // a wave range the fused kernel could not resolve: the two-kernel chain from the start
+    auto fallback = [&]() {
+        const int rc = encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, s, out_tokens, flags | kEncodeNoFused);
+        t_last_fused = 2;
+        return rc;
+    };
+    t_last_fused = fused ? 1 : 0;
     uint64_t rec[4] = {0, 0, 0, 0};
-    if (h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1) {
+    if (bounded) {
         // a bounded chain (no value can be made from itself): u16 passes 1 .. depth - 1 are all a
         // pass can need, enqueued without reading the device's pass count; passes after the one
         // that marks the fixpoint return at once, and a last kernel picks the final pass's total
@@ -772,6 +834,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = chain_sticky(h, ws, L, k_last)) return rc;
+        if (fused && (rec[2] >> 32)) return fallback();
         const uint32_t kd = (uint32_t)rec[2];
         t_last_u16_passes = kd ? (kd & ~blt::kDoneBytePass) : k_last;
         *out_tokens = rec[3];
@@ -789,6 +852,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
+        if (fused && (rec[2] >> 32)) return fallback();
         if ((uint32_t)rec[2]) break;
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
     }
@@ -1355,6 +1419,11 @@ uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0
 // contexts even where several share a device (on a one-GPU box: every context's producer and drain
 // threads, sharing the device); 0 restores one context per device.
 void blt_debug_set_shared_contexts(int on) { g_shared_contexts.store(on ? 1 : 0, std::memory_order_relaxed); }
+
+// Test hook: 0 runs every general map on the two-kernel chain, 1 (default) lets eligible maps fuse
+// passes 1 and 2.
+void blt_debug_set_fused(int on) { g_fused.store(on ? 1 : 0, std::memory_order_relaxed); }
+uint32_t blt_debug_last_fused() { return t_last_fused; }
 
 // Not in the public header: num_cpus::get() over a given cgroup root, /proc/self/cgroup file and
 // logical CPU count (tests: fake cgroup trees).

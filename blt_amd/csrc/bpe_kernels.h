@@ -60,6 +60,8 @@ struct PassParams {
                                // marks a merge valued its own first byte
     uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
                                // error bits in ctl[1], so the handle's next call fails
+    uint32_t* fused_fail;      // fused passes 1 + 2: set to 1 when a wave range's halo holds no
+                               // restart (the host then runs the two-kernel chain instead)
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
@@ -81,6 +83,13 @@ constexpr uint32_t kDoneBytePass = 0x80000000u;
 // p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
 // at least kTokRange tokens.
 hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
+// Passes 1 and 2 of a general map in one kernel (seg::scan_tokens_kernel<kHash, true>): bytes in,
+// the second pass's big-endian tokens out, for maps whose bucket table fits in LDS and chunk sizes
+// >= kMinChunkBytes.  A wave range takes the first pass's carry-in from the 64 bytes before it
+// (a greedy pass restarts after every pair it does not merge); the second pass's carries and every
+// offset go through the u16 scan's look-back.  Writes p.total, p.chunk_off and p.done as u16 pass
+// p.pass_id (1), or sets *p.fused_fail.
+hipError_t launch_scan_fused(const PassParams& p, int device, hipStream_t s);
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 // The end of a general map's chain enqueued up to its known depth: the final pass (the done word's,
 // else k_last) gives *tot_final and, when it wrote off1, the caller's chunk offsets.

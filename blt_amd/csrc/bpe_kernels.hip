@@ -1860,10 +1860,12 @@ __device__ __forceinline__ uint32_t tok_get(const PassParams& p, uint32_t tab, u
 // component (value word bit 30: a pass with no such merge leaves no mergeable pair behind, see
 // scan_tokens_kernel).  rem: tokens from the range start to the buffer end; cwl: low word of the
 // range's chunk-map word.
+// next_ok (fused passes): the token after position rem - 1 is valid (it is the next wave range's
+// first token, staged at position rem), so position rem - 1 may merge with it.
 template <int kHash>
 __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab, const uint32_t (&x)[8],
                                                uint32_t nxt, uint32_t rem, uint32_t cwl, int lane, int j,
-                                               TileStateT<kSt>& st, uint32_t& live) {
+                                               TileStateT<kSt>& st, uint32_t& live, bool next_ok = false) {
     // next lane's first token (wave_shl:1); lane 63 keeps the token after the wave's range
     const uint32_t nbw = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt, (int)x[0], 0x130, 0xF, 0xF, false);
     uint32_t r[16];
@@ -1890,8 +1892,8 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
     if (rem <= kWavePos || has_end) {   // uniform; rare
         const int32_t rr = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
-        uint32_t mm = m & ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u));
-        uint32_t forced = (rr >= 1 && rr <= 16) ? (1u << (rr - 1)) : 0u;   // the buffer's last token
+        uint32_t mm = m & (next_ok ? vmask : ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u)));
+        uint32_t forced = (!next_ok && rr >= 1 && rr <= 16) ? (1u << (rr - 1)) : 0u;   // the buffer's last token
         if (has_end) {                                                     // a chunk's last token
             const uint32_t e = ((cwl >> 12) & 0x7FFu) - 16u * (uint32_t)lane;
             if (e < 16u) { mm &= ~(1u << e); forced |= 1u << e; }
@@ -1926,7 +1928,8 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
 // rem: tokens from the range start to the buffer end; wtok: the range's first input token.
 __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uint32_t rem, uint32_t cwl, uint32_t cwh,
                                          int lane, int j, const TileStateT<kSt>& st, const uint32_t* gin,
-                                         uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave, bool has_coff) {
+                                         uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave, bool has_coff,
+                                         bool inplace = true) {
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
@@ -1955,7 +1958,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
-    if (wcnt == (rem < kWavePos ? rem : kWavePos) && O + goff == wtok) return;
+    if (inplace && wcnt == (rem < kWavePos ? rem : kWavePos) && O + goff == wtok) return;
     // one part: the stage holds the range's at most 1024 tokens
     const uint32_t x0 = wave * (uint32_t)kStageTok;   // the wave's stage, logical bytes
     stage_b16_pad(st.v[j], L, stg, x0 + (gb & 15u) + 2u * lane_off);
@@ -1965,7 +1968,230 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     copy_store<kCopyBlkTok, false>(ro, cp, lane, d);   // (branch-free here: f2 +2.5 %)
 }
 
+// ===========================================================================================
+// Passes 1 and 2 of a general map in one kernel (kFused): the u16 scan kernel with a front end that
+// runs the first pass on each wave range's 1024 bytes.  The first pass restarts after every byte
+// pair it does not merge (L[i + 1] = 1 when m[i] = 0), so a wave range's carry-in (does its first
+// byte land) follows from the 64 bytes before it: the last restart there lands, and the positions
+// after it alternate while every pair merges (tools/halo_model.py checks the rule against whole
+// passes).  The range's first-pass tokens go through the wave's stage into 16 tokens per lane,
+// followed by the next range's first token; from there the second pass is the u16 scan as it is
+// (its carries and all offsets through the look-back).  The intermediate tokens never leave LDS.
+// A range whose halo holds no restart (a run of merging pairs longer than the halo) sets
+// *p.fused_fail and the done word, and the host runs the two-kernel chain instead.
+// ===========================================================================================
+constexpr uint32_t kHalo = 64;   // bytes before a wave range, one per lane
+
+// Bytes 2h and 2h + 1 of word xw (h & 1 picks the word's half) as two big-endian u16 tokens.
+__device__ __forceinline__ uint32_t be_pair(uint32_t xw, int h) {
+    return __builtin_amdgcn_perm(xw, xw, (h & 1) ? 0x030C020Cu : 0x010C000Cu);
+}
+
+// Lane function of one wave range (lane_wave_fns' first part): the exclusive prefix word under
+// both wave carry-in hypotheses, no wave-function record.
+__device__ __forceinline__ uint32_t lane_ex1(uint32_t m, uint32_t vm) {
+    const uint64_t nonid = __ballot(m != 0xFFFFu);
+    const uint32_t mc = (m & ~1u) | (m << 16);
+    const uint32_t sst = mc & ~pk_shl1(mc);
+    const uint32_t rodd = mc & ~pk_add(mc, sst & 0xAAAAAAAAu);
+    const uint32_t M = (mc & ~rodd & 0x55555555u) | (rodd & 0xAAAAAAAAu);
+    const uint32_t L = ~(pk_shl1(M) | 1u) & (vm | (vm << 16));
+    const uint32_t cnt0 = __popc(L & 0xFFFFu), cnt1 = __popc(L >> 16);
+    const uint64_t cmask = __ballot(((M >> 31) & 1u) == 0u);
+    const uint64_t D = cmask & nonid, Mi = ~nonid, A = D << 1;
+    const uint64_t Y = ((Mi + A) ^ Mi ^ A) | A;
+    const uint64_t F = nonid ? ((nonid & (0ull - nonid)) << 1) - 1ull : ~0ull;
+    const uint64_t CI0 = Y, CI1 = Y | F;
+    const uint32_t packed = lane_sel(CI0, cnt0, cnt1) | (lane_sel(CI1, cnt0, cnt1) << 16);
+    const uint32_t incl = wave_scan(packed);
+    return (incl - packed) | lane_sel(CI0, 0u, 0x8000u) | lane_sel(CI1, 0u, 0x80000000u);
+}
+
+// A lane's landing mask L, merge starts M and token offset under wave carry-in C (1: the range's
+// first position lands), as emit_tok derives them.
+__device__ __forceinline__ void lands1(uint32_t m, uint32_t vmask, uint32_t ex, uint32_t C, uint32_t& L,
+                                       uint32_t& M, uint32_t& off) {
+    const uint32_t c = __builtin_amdgcn_ubfe(ex, 16u * C + 15u, 1);
+    off = __builtin_amdgcn_ubfe(ex, 16u * C, 15);
+    const uint32_t mc = c ? m : (m & ~1u);
+    const uint32_t sst = mc & ~(mc << 1);
+    const uint32_t rodd = mc & ~(mc + (sst & 0xAAAAu));
+    M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
+    L = ~((M << 1) | (c ^ 1u)) & vmask;
+}
+
+// Bytes of tile Tn for the fused kernel: a lane's 16 bytes (x[j][0..3]), its halo byte (x[j][4]:
+// byte wb - 64 + lane of its wave range wb) and the 4 bytes after the range (nxt[j]); exact byte
+// loads near the buffer end (as load_tile).
+__device__ __forceinline__ void load_fused(const PassParams& p, uint64_t n, uint32_t Tn, uint32_t wave, int lane,
+                                           uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt]) {
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
+    const uint64_t tile0 = (uint64_t)Tn * kTileTok;
+    const uint64_t left = n > tile0 ? n - tile0 : 0;
+    const __amdgpu_buffer_rsrc_t rd = rsrc_at(in + tile0, left & ~3ull);
+#pragma unroll
+    for (int j = 0; j < kSt; ++j) {
+        const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(wrel + 16u * (uint32_t)lane), 0, BLT_LDPOL);
+        x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(wrel + kWavePos), 0, 0);
+        const uint64_t wb = tile0 + wrel;
+        x[j][4] = 0u;
+        if (wb >= kHalo)   // uniform
+            x[j][4] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc_at(in + wb - kHalo, kHalo), lane, 0, 0);
+    }
+    const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
+#pragma unroll
+    for (int j = 0; j < kSt; ++j) {
+        const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
+        if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
+            const __amdgpu_buffer_rsrc_t r = rsrc_at(in + tile0, left);
+            uint32_t nw = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                nw |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(wrel + kWavePos) + b, 0, 0) << (8 * b);
+            nxt[j] = nw;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t d = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    d |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(wrel + 16u * (uint32_t)lane) + 4 * q + b, 0, 0)
+                         << (8 * b);
+                x[j][q] = d;
+            }
+        }
+    }
+}
+
+// Front end of one wave range [wb, wb + 1024) of bytes: the first pass, its tokens compacted
+// through the wave's stage into x (16 per lane) with the next range's first token after them, and
+// the second pass's inputs: nxt (that token), rem2 (tokens of the range; 2048 when it holds 1024
+// and the next token is valid), next_ok, and the range's chunk-map word (cwl, cwh) in token
+// positions.  Wave-uniform control throughout.
 template <int kHash>
+__device__ __forceinline__ void fused_front(const PassParams& p, uint32_t tab, uint32_t (&x)[8], uint32_t& nxt,
+                                            uint64_t wb, uint64_t n, int lane, uint32_t wave, uint8_t* stg,
+                                            uint32_t& rem2, bool& next_ok, uint32_t& cwl, uint32_t& cwh, uint32_t& C2) {
+    const uint32_t hb = x[4] & 0xFFu;
+    const uint32_t nb4 = nxt;
+    const uint64_t left = n > wb ? n - wb : 0;
+    const uint32_t rem1 = (uint32_t)(left > 2u * kWavePos ? 2u * kWavePos : left);
+    // chunk geometry: wb = q cs + r; the first chunk start at or after wb is s bytes on
+    const uint64_t cs = p.cs;
+    uint64_t q = __umul64hi(wb, p.cs_magic);
+    uint64_t r = wb - q * cs;
+    if (r >= cs) { q += 1; r -= cs; }
+    if (r >= cs) { q += 1; r -= cs; }
+    const uint64_t s = r ? cs - r : 0;
+    uint32_t cwl1 = 0;
+    if (s < kWavePos) cwl1 |= kCmStart | (uint32_t)s;
+    if (r && s >= 1 && s <= kWavePos) cwl1 |= kCmEnd | ((uint32_t)(s - 1) << 12);
+
+    // first pass over the range's bytes as big-endian tokens
+    uint32_t t[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) t[h] = be_pair(x[h >> 1], h);
+    TileStateT<kSt> s1;
+    uint32_t live1 = 0;
+    const uint32_t m1 = phase1_tok<kHash>(p, tab, t, (nb4 & 0xFFu) << 8, rem1, cwl1, lane, 0, s1, live1);
+    const uint32_t vm1 = s1.mv[0] >> 16;
+    const uint32_t ex1 = lane_ex1(m1, vm1);
+
+    // Carries from the halo (lane l: byte wb - 64 + l).  Pass 1: the last restart (a byte whose
+    // left pair does not merge, or a chunk start) lands and the merging pairs after it alternate, so
+    // C1 = 1 unless byte wb - 1 lands and merges with byte wb.  Pass 2 the same way over the halo's
+    // first-pass tokens after its first restart, up to the range's first token: C2 = 1 unless the
+    // halo's last first-pass token lands in pass 2 and merges with it.  A halo with no restart for
+    // either pass cannot resolve the range.
+    uint32_t C1 = 1u;
+    C2 = 1u;
+    if (wb != 0 && r != 0 && left != 0) {
+        const uint32_t b0 = uni(lane_u32(x[0], 0)) & 0xFFu;   // byte wb: lane 63's right neighbour
+        const uint32_t hn = (uint32_t)__builtin_amdgcn_update_dpp((int)b0, (int)hb, 0x130, 0xF, 0xF, false);
+        const int cl = r <= kHalo ? (int)kHalo - (int)r : -1;   // a chunk start in the halo, at lane cl
+        const uint32_t v1 = lane + 1 != cl ? tok_get<kHash>(p, tab, (hb << 8) | (hn << 24)) : 0u;
+        const bool hit = (v1 >> 31) != 0u;
+        const uint64_t hm = __ballot(hit);
+        const uint64_t below = (2ull << lane) - 1ull;   // lanes 0..lane (lane 63: all)
+        const bool rst = lane == cl || (lane >= 1 && ((hm >> (lane - 1)) & 1ull) == 0ull);
+        const uint64_t R = __ballot(rst);
+        bool ok = R != 0;
+        if (ok) {
+            const int lr = 63 - __clzll(R);
+            C1 = (((63 - lr) & 1) == 0 && ((hm >> 63) & 1ull)) ? 0u : 1u;
+            // first-pass landings from the first restart on, and their tokens
+            const int r0 = __builtin_ctzll(R);
+            const uint64_t rl = R & below;
+            const bool land = lane >= r0 && rl != 0 && ((lane - (63 - __clzll(rl))) & 1) == 0;
+            const uint64_t LM = __ballot(land);
+            const uint32_t t1 = hit ? (v1 & 0xFFFFu) : (hb << 8);
+            const uint32_t tf = uni(lane_u32(C1 ? (s1.v[0][0] & 0xFFFFu) : (s1.v[0][0] >> 16), 0));   // range's first token
+            const int nl = lane + 1 + (hit ? 1 : 0);   // next landing (for a landing lane)
+            uint32_t tn = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (nl < 64 ? nl : 63), (int)t1);
+            if (nl >= 64) tn = tf;
+            const uint32_t v2 = (land && nl != cl) ? tok_get<kHash>(p, tab, t1 | (tn << 16)) : 0u;
+            const uint64_t H2 = __ballot((v2 >> 31) != 0u);
+            const uint64_t lprev = LM & (below >> 1);   // landings below this lane
+            const bool rst2 = land && (lane == cl || (lprev != 0 && ((H2 >> (63 - __clzll(lprev))) & 1ull) == 0ull));
+            const uint64_t R2 = __ballot(rst2);
+            ok = R2 != 0;
+            if (ok) {
+                const int lr2 = 63 - __clzll(R2), lst = 63 - __clzll(LM);   // last restart, last landing
+                const uint64_t span = (lst == 63 ? ~0ull : ((2ull << lst) - 1ull)) & ~((1ull << lr2) - 1ull);
+                const bool l2 = ((__popcll(LM & span) - 1) & 1) == 0;   // the last landing lands in pass 2
+                C2 = (l2 && ((H2 >> lst) & 1ull)) ? 0u : 1u;
+            }
+        }
+        if (!ok) {   // no restart: this kernel cannot resolve the range (the host falls back)
+            if (lane == 0) {
+                *KARG(fused_fail) = 1u;
+                if (uint32_t* dn = KARG(done)) *dn = p.pass_id;
+            }
+        }
+    }
+    uint32_t L1, M1, off1;
+    lands1(m1, vm1, ex1, C1, L1, M1, off1);
+    const uint32_t c1 = uni(lane_u32(off1 + __popc(L1), 63));
+
+    // the next range's first token (the first landing at or after wb + 1024)
+    const uint32_t Cn = (uni(lane_u32(M1, 63)) >> 15) & 1u;   // 1: byte wb + 1024 merged into our last token
+    const uint64_t fnx = wb + kWavePos + Cn;
+    next_ok = fnx < n && !(r != 0 && s == (uint64_t)kWavePos + Cn);
+    uint32_t tokn = 0;
+    if (next_ok) {
+        const uint32_t a = (nb4 >> (8 * Cn)) & 0xFFu, b = (nb4 >> (8 * (Cn + 1))) & 0xFFu;
+        const bool pv = fnx + 1 < n && !(r != 0 && s == (uint64_t)kWavePos + Cn + 1);
+        const uint32_t v = pv ? tok_get<kHash>(p, tab, (a << 8) | (b << 24)) : 0u;
+        tokn = (v >> 31) ? (v & 0xFFFFu) : (a << 8);
+    }
+
+    // compaction through the stage, the next token after the range's tokens, 16 tokens per lane back
+    const uint32_t x0 = wave * (uint32_t)kStageTok;
+    stage_b16_pad(s1.v[0], L1, stg, x0 + 2u * off1);
+    if (next_ok && lane == 0) *reinterpret_cast<uint16_t*>(stg + stage_phys(x0 + 2u * c1)) = (uint16_t)tokn;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint2 d = *reinterpret_cast<const uint2*>(stg + stage_phys(x0 + 32u * (uint32_t)lane + 8u * k));
+        x[2 * k] = d.x;
+        x[2 * k + 1] = d.y;
+    }
+    nxt = tokn;
+    rem2 = (c1 == kWavePos && next_ok) ? 2u * kWavePos : c1;
+
+    // chunk start of this range in token positions (it lands: the pair before it is cut)
+    cwl = 0u;
+    cwh = 0u;
+    if (s < kWavePos && s < left) {
+        const uint32_t sl = (uint32_t)s >> 4, sb = (uint32_t)s & 15u;
+        const uint32_t te = uni(__builtin_amdgcn_readlane((int)(off1 + __popc(L1 & ((1u << sb) - 1u))), (int)sl));
+        cwl = kCmStart | te;
+        if (s != 0 && te != 0) cwl |= kCmEnd | ((te - 1u) << 12);
+        cwh = (uint32_t)(r ? q + 1 : q);
+    }
+}
+
+template <int kHash, bool kFused = false>
 __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     constexpr bool kHashLds = kHash != 0;
     extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
@@ -1979,11 +2205,11 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     __shared__ uint32_t s_p1cnt[kRing];
     __shared__ uint32_t s_rdone, s_lbdone, s_tkdone;
 
-    if (pass_done(p)) return;   // an earlier pass merged nothing (uniform over the grid)
+    if (!kFused && pass_done(p)) return;   // an earlier pass merged nothing (uniform over the grid)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = uni((uint32_t)tid >> 6);
-    const uint64_t n = uni64(token_count(p));
+    const uint64_t n = kFused ? p.n : uni64(token_count(p));   // fused: bytes
     const bool has_coff = p.chunk_off != nullptr;
     const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
     // the grid was sized for the token bound; workgroups past the tiles the previous pass left leave
@@ -2028,7 +2254,10 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca[kSt][2], cb[kSt][2];
 #pragma unroll
     for (int j = 0; j < kSt; ++j) { na[j] = nb[j] = 0u; ca[j][0] = ca[j][1] = cb[j][0] = cb[j][1] = 0u; }
-    if (T < ntiles) load_tok(p, n, T, wave, lane, xa, na, ca);
+    if (T < ntiles) {
+        if constexpr (kFused) load_fused(p, n, T, wave, lane, xa, na);
+        else load_tok(p, n, T, wave, lane, xa, na, ca);
+    }
     TileStateT<kSt> sa, sb;
     uint64_t lbs[kLbWin];
     uint32_t it = 0;
@@ -2046,8 +2275,14 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
         if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
         uint32_t cwl[kSt], cwh[kSt];
 #pragma unroll
-        for (int j = 0; j < kSt; ++j) { cwl[j] = uni(cw[j][0]); cwh[j] = uni(cw[j][1]); }
-        if (Tq < ntiles) load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
+        for (int j = 0; j < kSt; ++j) {
+            cwl[j] = kFused ? 0u : uni(cw[j][0]);   // fused: from the front end
+            cwh[j] = kFused ? 0u : uni(cw[j][1]);
+        }
+        if (Tq < ntiles) {
+            if constexpr (kFused) load_fused(p, n, Tq, wave, lane, xq, nxtq);
+            else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
+        }
         uint32_t tk = kNone;
         if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
@@ -2056,10 +2291,48 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
         if (T < ntiles) {
             if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
             uint32_t m[kSt], live = 0;
+            uint32_t rem2[kSt], C2[kSt];
+            bool nok[kSt];
+            if constexpr (kFused) {
 #pragma unroll
-            for (int j = 0; j < kSt; ++j)
-                m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
-            lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], __ballot(live) != 0 ? 1u : 0u);
+                for (int j = 0; j < kSt; ++j)
+                    fused_front<kHash>(p, tab, x[j], nxt[j], (uint64_t)T * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos,
+                                       n, lane, wave, s_stage, rem2[j], nok[j], cwl[j], cwh[j], C2[j]);
+#pragma unroll
+                for (int j = 0; j < kSt; ++j)
+                    m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem2[j], cwl[j], lane, j, sc, live, nok[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < kSt; ++j)
+                    m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
+            }
+            const uint32_t wl = __ballot(live) != 0 ? 1u : 0u;
+            lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], wl);
+            if constexpr (kFused) {
+                // a fused range knows its carry-in (C2, from the halo): its wave function is the
+                // constant one, with the count under C2 and the carry into the next range (the
+                // range's tokens fill only its first rem2 positions, so the lane functions' own
+                // carry-out, past the unused positions, is not it)
+#pragma unroll
+                for (int j = 0; j < kSt; ++j) {
+                    uint32_t L2, M2, off2;
+                    lands1(m[j], sc.mv[j] >> 16, sc.ex[j], C2[j], L2, M2, off2);
+                    const uint32_t cnt = uni(lane_u32(off2 + __popc(L2), 63));
+                    uint32_t co = 1u;
+                    if (nok[j]) {
+                        const uint32_t last = (rem2[j] > kWavePos ? kWavePos : rem2[j]) - 1u;
+                        const uint32_t mb = uni(__builtin_amdgcn_readlane((int)M2, (int)(last >> 4)));
+                        co = ((mb >> (last & 15u)) & 1u) ? 0u : 1u;
+                    }
+                    if (lane == 63) {
+                        const uint32_t g = (uint32_t)j * kWaves + wave;
+                        s_wfn[slot][g][0] = wl << 1;
+                        s_wfn[slot][g][1] = co;
+                        s_wfn[slot][g][2] = cnt;
+                        s_wfn[slot][g][3] = cnt;
+                    }
+                }
+            }
             __builtin_amdgcn_s_setprio(0);
             uint32_t old = 0;
             if (lane == 0)
@@ -2124,8 +2397,8 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
 #pragma unroll
                 for (int j = 0; j < kSt; ++j) {
                     const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
-                    emit_tok(p, wtok, rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
-                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff);
+                    emit_tok(p, wtok, kFused ? 0u : rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
+                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff, !kFused);
                 }
             }
             __builtin_amdgcn_s_setprio(0);
@@ -2246,7 +2519,7 @@ __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
 // per (device, kernel) and cached in atomics (launchers run concurrently from many host threads).
 struct GridCache {
     std::atomic<int> cus[64];
-    std::atomic<int> occ[64][8];
+    std::atomic<int> occ[64][16];
 };
 static GridCache g_grid;   // zero-initialised (static storage)
 static int grid_for(uint32_t ntiles, int device, const void* fn, int threads, int kernel_id) {
@@ -2347,6 +2620,20 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
     if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2>), g, b, smem, s, p);
     else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1>), g, b, smem, s, p);
     else hipLaunchKernelGGL((seg::scan_tokens_kernel<0>), g, b, 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_fused(const PassParams& p, int device, hipStream_t s) {
+    if (p.n == 0) return hipSuccess;
+    if (p.hbytes > kHashLdsMax || p.cs < kMinChunkBytes || !p.fused_fail) return hipErrorInvalidValue;
+    const int mode = p.hone ? 2 : 1;
+    const void* fn = mode == 2 ? (const void*)seg::scan_tokens_kernel<2, true> : (const void*)seg::scan_tokens_kernel<1, true>;
+    const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
+    const int grid = grid_for(ntiles, device, fn, seg::kThreads, 8 + mode);
+    const size_t smem = ((size_t)p.hbytes + 1023) & ~(size_t)1023;
+    const dim3 g((unsigned)grid), b(seg::kThreads);
+    if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2, true>), g, b, smem, s, p);
+    else hipLaunchKernelGGL((seg::scan_tokens_kernel<1, true>), g, b, smem, s, p);
     return hipGetLastError();
 }
 
