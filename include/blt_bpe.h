@@ -165,7 +165,10 @@ size_t blt_bpe_workspace_size(const blt_bpe *h, uint64_t n, uint64_t chunk_size)
  * work (no host synchronisation) for every single-pass map and for every general map whose merge
  * chains are bounded (no value can be made from itself: its passes are known up front).  A
  * general map with a cycle (e.g. (97, 98) -> 97) waits for the stream after its first u16 pass
- * and then after every 4, to read whether the chain has reached its fixpoint. */
+ * and then after every 4, to read whether the chain has reached its fixpoint.  A general map whose
+ * bucket table fits in LDS (and that has a key with a token component) runs its first two passes
+ * in one kernel whenever the call waits anyway (out_tokens given, or a cyclic map), falling back
+ * to two kernels for input the fused kernel cannot resolve; the output is the same either way. */
 int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
                           uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
                           void *stream, uint64_t *out_tokens);
