@@ -259,6 +259,9 @@ struct blt_bpe {
     // A general map whose keys are all byte pairs: its first pass reports whether it made a token
     // below 256 (the only key components), and is the fixpoint when it made none.
     bool live_first = false;
+    // A byte-pair key (a, a): a run of that byte merges pair after pair, so the fused first two
+    // passes could find no restart in a wave range's halo; such maps keep the two-kernel chain.
+    bool byte_self_pair = false;
     // General map: the longest merge chain (chain_depth; 0 = unbounded): the passes it needs are
     // known up front, so they are enqueued without reading the device's pass count.
     uint32_t chain_depth = 0;
@@ -456,6 +459,7 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
     for (const auto& kv : map) {
         const uint32_t a = kv.first >> 16, b = kv.first & 0xFFFF;
         if (a < 256 && b < 256) {
+            if (a == b) h->byte_self_pair = true;
             if (kv.second == a) self_valued = true;
             if (kv.second < 256) hi_merge = false;
             hi_used[kv.second >> 8] = 1;
@@ -792,6 +796,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // keep the byte pass, which can); its halo fallback is read where the host reads the chain's
     // totals anyway, so an async bounded chain keeps the two-kernel path.
     const bool fused = !(flags & kEncodeNoFused) && g_fused.load(std::memory_order_relaxed) && !h->live_first &&
+                       !h->byte_self_pair &&
                        h->hwords.size() * sizeof(uint32_t) <= blt::kHashLdsMax && cs >= blt::kMinChunkBytes &&
                        (!bounded || out_tokens != nullptr);
     uint32_t* fused_fail = reinterpret_cast<uint32_t*>(ws + L.total + 20);   // beside the done word
@@ -801,6 +806,20 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (int rc = run_fused(h, t, dev, s, ws, L, d_in, n, cs, d_out, off[1], tot + 1, done, fused_fail)) return rc;
         cur = 1;
         k = 2;
+        if (bounded && h->chain_depth > 2) {
+            // more passes to enqueue: see first whether the fused kernel resolved every range (a
+            // failed one leaves them no-ops, but each costs its launch)
+            uint32_t ff = 0;
+            HIP_TRY(hipMemcpyAsync(&ff, fused_fail, sizeof ff, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (int rc = chain_sticky(h, ws, L, 1)) return rc;
+            if (ff) {
+                const int rc = encode_device(h, d_in, n, cs, d_out, d_chunk_off, d_ws, ws_bytes, s, out_tokens,
+                                             flags | kEncodeNoFused);
+                t_last_fused = 2;
+                return rc;
+            }
+        }
     } else {   // pass 1 (pass id 0): with byte-pair keys it marks itself final when it made no key component
         const Chain c0{nullptr, tot, done, 0};
         if (int rc = run_pass(h, t, dev, s, ws, L, d_in, false, n, cs, nullptr, d_out, true, 2 * n, off[0], true, &c0))

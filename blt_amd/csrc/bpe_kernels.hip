@@ -2147,6 +2147,9 @@ __device__ __forceinline__ void fused_front(const PassParams& p, uint32_t tab, u
             if (lane == 0) {
                 *KARG(fused_fail) = 1u;
                 if (uint32_t* dn = KARG(done)) *dn = p.pass_id;
+                // fail fast: every later ticket claim gets a tile past the end, so the workgroups
+                // finish the tiles they hold (all of whose predecessors are claimed) and leave
+                atomicMax(KARG(ctl), 0x80000000u);
             }
         }
     }

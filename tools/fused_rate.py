@@ -2,7 +2,7 @@
 default): synchronous encode_device (the token count read back), host wall clock, median of reps,
 output checked bit-exact against the oracle.  Prints one JSON line per mode.
 
-    python tools/fused_rate.py [--mib 256] [--reps 20] [--map multi|selfval]
+    python tools/fused_rate.py [--mib 256] [--reps 20] [--map multi|selfval|chain]
 """
 import argparse
 import json
@@ -28,8 +28,12 @@ def main():
     from oracle import oracle as O
     cs = 16 << 20
     n = a.mib << 20
-    host = synth.text(n, seed=2)
-    m = synth.CHAINED_TEXT_MAP if a.map == "multi" else synth.SELF_VALUED_MAP
+    if a.map == "chain":   # bench.py's `chain` row: runs of 'a', a 24-level doubling chain
+        host = np.full(n, 97, np.uint8)
+        m = synth.doubling_chain(24)
+    else:
+        host = synth.text(n, seed=2)
+        m = synth.CHAINED_TEXT_MAP if a.map == "multi" else synth.SELF_VALUED_MAP
     s = blt_amd.BpeStrategy(m)
     d_in = torch.from_numpy(host).cuda()
     d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
