@@ -295,11 +295,13 @@ def pmc_traffic(path, wl, n):
         return None, "no record"
     with open(path) as f:
         tj = json.load(f)
-    tw = tj.get("workloads", {}).get(wl, {})
-    if not tw:
+    recs = [r for k, r in tj.get("workloads", {}).items() if r.get("workload", k) == wl]
+    if not recs:
         return None, f"no {wl} record"
-    if tw.get("bytes_per_gpu") != n or tw.get("chunk_size") != CHUNK:
+    sized = [r for r in recs if r.get("bytes_per_gpu") == n and r.get("chunk_size") == CHUNK]
+    if not sized:
         return None, "record is for another size"
+    tw = sized[0]
     if tw.get("kernel_source_sha256") != kernel_source_sha():
         return None, "record is for another kernel build (kernel_source_sha256 differs)"
     return tw.get("hbm_bytes_per_launch"), tw.get("source")
