@@ -1167,6 +1167,35 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
     return 0;
 }
 
+// How blt_bpe_process_chunks runs n bytes on n_gpus: device contexts, and the single-staging path
+// (encode_host_on) or the windowed one (encode_host_multi).
+struct HostPlan {
+    std::vector<int> devs;
+    bool multi = false;
+};
+int host_plan(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus, HostPlan* plan) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return fail(BLT_E_NODEV, "no HIP device available");
+    const uint64_t nchunks = (n + cs - 1) / cs;
+    // n_gpus device contexts; context d runs on device d % (visible devices), so more contexts than
+    // devices share devices (each its own threads and streams).  Windows of whole chunks go to the
+    // contexts round-robin and land at their final output offsets in chunk order (encode_host_multi).
+    uint64_t g = (uint64_t)std::max(1, std::min(n_gpus < 1 ? 1 : n_gpus, kMaxDevices));
+    g = std::min<uint64_t>(g, nchunks);
+    // Contexts that would share a device add only contention for its DMA engines and PCIe link
+    // (measured on one MI355X: 8 contexts 29.8 GB/s against 45 GB/s for one): one context per
+    // device unless a test asks for every shard's own context (blt_debug_set_shared_contexts).
+    if (!g_shared_contexts.load(std::memory_order_relaxed)) g = std::min<uint64_t>(g, (uint64_t)count);
+    plan->devs.assign(g, 0);
+    plan->multi = !(g == 1 && !(h->single_pass && n > kPipeWindow && cs <= kPipeWindow / 2));
+    if (g == 1) {
+        if (int rc = current_device(&plan->devs[0])) return rc;
+    } else {
+        for (uint64_t r = 0; r < g; ++r) plan->devs[r] = (int)(r % (uint64_t)count);
+    }
+    return 0;
+}
+
 }  // namespace
 
 // ===========================================================================================
@@ -1520,6 +1549,48 @@ int blt_basic_process_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t ou
     )
 }
 
+}  // extern "C"
+
+// Device setup ahead of a blt_bpe_process_chunks(h, ., n, cs, n_gpus) call (blt_run_tokenizer runs
+// it beside the input's mmap): HIP start-up, the handle's device tables and the staging buffers
+// that call will use, left in the context pool.  Failures are left for the call itself to report.
+void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) try {
+    if (!h || !n || !cs) return;
+    HostPlan plan;
+    if (host_plan(h, n, cs, n_gpus, &plan) != 0) return;
+    const uint64_t g = plan.devs.size();
+    const uint64_t nchunks = (n + cs - 1) / cs;
+    const uint64_t share = (nchunks + g - 1) / g * cs;
+    const uint64_t win = h->single_pass ? std::max<uint64_t>(cs, std::min<uint64_t>(kPipeWindow / cs * cs, share)) : share;
+    const uint64_t per_ctx = ((n + win - 1) / win + g - 1) / g;
+    const int slots = (int)std::min<uint64_t>(kPipeSlots, per_ctx);
+    (void)sticky_word(h);
+    for (uint64_t d = 0; d < g; ++d) {
+        const int dev = plan.devs[d];
+        if (hipSetDevice(dev) != hipSuccess) return;
+        DevTables* t;
+        if (device_tables(h, dev, &t) != 0) return;
+        DevCtx* c = ctx_acquire(dev);
+        if (!c) return;
+        CtxGuard guard{c};
+        if (plan.multi) {
+            for (int k = 0; k < slots; ++k)
+                if (pipe_slot_ready(h, c->pipe[k], std::min(win, n), cs) != 0) return;
+        } else {
+            const WsLayout L = ws_layout(h->single_pass, n, cs);
+            uint8_t* offp = reinterpret_cast<uint8_t*>(c->d_off);
+            if (grow(&c->d_in, &c->in_cap, up16(n)) || grow(&c->d_out, &c->out_cap, up16(2 * n)) ||
+                grow(&c->d_ws, &c->ws_cap, L.bytes) || grow(&offp, &c->off_cap, 8 * (L.nchunks + 1)))
+                return;
+            c->d_off = reinterpret_cast<uint64_t*>(offp);
+        }
+    }
+    if (g == 1 && !plan.multi) (void)hipSetDevice(plan.devs[0]);
+} catch (...) {
+}
+
+extern "C" {
+
 int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t cs, int n_gpus, uint8_t* out,
                            size_t out_cap, size_t* out_len, uint64_t* chunk_out_len) {
     GUARDED(
@@ -1529,32 +1600,15 @@ int blt_bpe_process_chunks(const blt_bpe* h, const uint8_t* in, size_t n, size_t
     if (int rc = sticky_check(h)) return rc;
     if (n == 0) return 0;
     if (out_cap < 2 * (uint64_t)n) return fail(BLT_E_NOSPC, "out_cap %zu < 2 * n", out_cap);
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count < 1) return fail(BLT_E_NODEV, "no HIP device available");
     const uint64_t nchunks = (n + cs - 1) / cs;
-    // n_gpus device contexts; context d runs on device d % (visible devices), so more contexts than
-    // devices share devices (each its own threads and streams).  Windows of whole chunks go to the
-    // contexts round-robin and land at their final output offsets in chunk order (encode_host_multi).
-    uint64_t g = (uint64_t)std::max(1, std::min(n_gpus < 1 ? 1 : n_gpus, kMaxDevices));
-    g = std::min<uint64_t>(g, nchunks);
-    // Contexts that would share a device add only contention for its DMA engines and PCIe link
-    // (measured on one MI355X: 8 contexts 29.8 GB/s against 45 GB/s for one): one context per
-    // device unless a test asks for every shard's own context (blt_debug_set_shared_contexts).
-    if (!g_shared_contexts.load(std::memory_order_relaxed)) g = std::min<uint64_t>(g, (uint64_t)count);
+    HostPlan plan;
+    if (int rc = host_plan(h, n, cs, n_gpus, &plan)) return rc;
     uint64_t total = 0;
     std::vector<uint64_t> offs;
-    if (g == 1 && !(h->single_pass && n > kPipeWindow && cs <= kPipeWindow / 2)) {
-        int dev;
-        if (int rc = current_device(&dev)) return rc;
-        if (int rc = encode_host_on(h, dev, in, n, cs, out, &total, chunk_out_len ? &offs : nullptr)) return rc;
+    if (!plan.multi) {
+        if (int rc = encode_host_on(h, plan.devs[0], in, n, cs, out, &total, chunk_out_len ? &offs : nullptr)) return rc;
     } else {
-        std::vector<int> devs(g);
-        if (g == 1) {
-            if (int rc = current_device(&devs[0])) return rc;
-        } else {
-            for (uint64_t r = 0; r < g; ++r) devs[r] = (int)(r % (uint64_t)count);
-        }
-        if (int rc = encode_host_multi(h, devs, in, n, cs, out, &total, chunk_out_len ? &offs : nullptr)) return rc;
+        if (int rc = encode_host_multi(h, plan.devs, in, n, cs, out, &total, chunk_out_len ? &offs : nullptr)) return rc;
     }
     if (chunk_out_len)
         for (uint64_t k = 0; k < nchunks; ++k) chunk_out_len[k] = 2 * (offs[k + 1] - offs[k]);

@@ -331,6 +331,13 @@ int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& s
     return 0;
 }
 
+}  // namespace
+
+// blt_host.cpp: device setup ahead of a blt_bpe_process_chunks call of this shape.
+void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus);
+
+namespace {
+
 int run(const blt_run_config* c) {
     if (!c) return set_error(BLT_E_INVALID_INPUT, "null config");
     if (c->chunk_size == 0) return set_error(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
@@ -341,11 +348,19 @@ int run(const blt_run_config* c) {
     else st.kind = Strategy::kBasic;
     st.h = c->bpe;
     st.gpus = c->n_gpus;
-    if (st.kind == Strategy::kBpe && st.gpus <= 0) {
-        int count = 0;
-        st.gpus = (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? count : 1;
-    }
     const size_t cs = (size_t)c->chunk_size;
+    // HIP start-up and the first window's device setup run on a helper thread while the input is
+    // mapped (BPE from a file): the device count, the handle's tables, staging buffers
+    std::thread prewarm;
+    auto gpu_count = [](int g) {
+        if (g > 0) return g;
+        int count = 0;
+        return (hipGetDeviceCount(&count) == hipSuccess && count > 0) ? count : 1;
+    };
+    struct Join {
+        std::thread& t;
+        ~Join() { if (t.joinable()) t.join(); }
+    } join_prewarm{prewarm};
 
     // setup_io (io_handler.rs:55-62): the input is opened and mapped first
     const bool timing = getenv("BLT_CLI_TIMING") != nullptr;
@@ -363,6 +378,14 @@ int run(const blt_run_config* c) {
             return os_error(e);
         }
         n = (size_t)sb.st_size;
+        if (st.kind == Strategy::kBpe && n && !getenv("BLT_NO_PREWARM")) {   // (env: A/B runs)
+            const size_t per = std::max<size_t>(1, (size_t(256) << 20) / cs);   // run_mmap's window
+            const uint64_t win = std::min<uint64_t>(n, (uint64_t)per * cs);
+            prewarm = std::thread([&st, &gpu_count, win, cs] {
+                st.gpus = gpu_count(st.gpus);
+                blt_prewarm_chunks(st.h, win, cs, st.gpus);
+            });
+        }
         if (n) {
             // MAP_POPULATE: fault the file in bulk up front, not page by page under the GPU copies
             void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
@@ -387,6 +410,8 @@ int run(const blt_run_config* c) {
         size_t n;
         ~Unmap() { if (p) munmap(const_cast<uint8_t*>(p), n); }
     } unmap{map, n};
+    if (prewarm.joinable()) prewarm.join();
+    else if (st.kind == Strategy::kBpe) st.gpus = gpu_count(st.gpus);
 
     // setup_output_writer (io_handler.rs:70-78): File::create truncates; None is stdout
     Sink sink;
