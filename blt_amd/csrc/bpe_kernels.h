@@ -16,6 +16,7 @@ constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chu
 constexpr uint64_t kTilePosBytes = BLT_TILE_BYTES;   // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
+constexpr uint32_t kCtlLeft = 15;             // ctl word: workgroups of a single-pass launch that have left
 
 // Parameters of one merge pass over a whole buffer of positions.
 struct PassParams {

@@ -171,6 +171,25 @@ __device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint
     }
 }
 
+// Self-reset of a single-pass launch: the last workgroup to leave zeroes the ticket and the
+// status words (every look-back is over by then), so the next launch on this workspace needs no
+// memset (BLT_ENCODE_WORKSPACE_ZEROED).  The error flags and first-error record stay.  Each
+// thread's stores are complete before its workgroup counts itself out, so a late status publish
+// cannot land after the zeroing.  flag: a workgroup-shared word the caller is done with.
+__device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles, uint32_t* flag) {
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *flag = __hip_atomic_fetch_add(p.ctl + kCtlLeft, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+    __syncthreads();
+    if (*flag) {
+        uint4* st = reinterpret_cast<uint4*>(p.status);   // 16-byte aligned (after the control block)
+        const uint32_t units = (ntiles + 1u) / 2u;         // within the zeroed region (rounded to 16 bytes)
+        for (uint32_t i = threadIdx.x; i < units; i += blockDim.x) st[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (threadIdx.x == 0) { p.ctl[0] = 0u; p.ctl[kCtlLeft] = 0u; }
+    }
+}
+
 // Lane i's 64-bit value from its two halves.  readlane returns int: cast each half to uint32_t
 // before widening, or the low half sign-extends over the flag and carry bits.
 __device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int i) {
@@ -576,6 +595,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
             __syncthreads();
         }
     }
+    if constexpr (kDense) self_reset(p, p.ntiles, &s_ticket);   // byte input: single-pass maps and pass 1
 }
 
 template <typename InT, bool kBE>
@@ -1707,6 +1727,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     }
     if (wg_rec && lane == 0)
         atomicMax(reinterpret_cast<unsigned long long*>(wg_rec + 2), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    self_reset(p, ntiles, &s_tkdone);
 }
 
 // ===========================================================================================

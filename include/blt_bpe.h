@@ -174,11 +174,16 @@ int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uin
                           void *stream, uint64_t *out_tokens);
 
 /* Flags of blt_bpe_encode_device_ex. */
-#define BLT_ENCODE_WORKSPACE_ZEROED 1u /* caller ran blt_bpe_workspace_reset on this stream since the
-                                          last encode (single-pass maps; ignored otherwise) */
+#define BLT_ENCODE_WORKSPACE_ZEROED 1u /* the workspace's look-back words are zero: the caller ran
+                                          blt_bpe_workspace_reset on this stream since the last encode,
+                                          or the last encode on it was a single-pass one (single-pass
+                                          maps; ignored otherwise) */
 
 /* As blt_bpe_encode_device, with flags.  With BLT_ENCODE_WORKSPACE_ZEROED the call enqueues only
- * the merge-scan kernel, so events around it time that kernel alone. */
+ * the merge-scan kernel, so events around it time that kernel alone.  A single-pass encode leaves
+ * the workspace's ticket and status words zeroed when its kernel ends (its last workgroup resets
+ * them), so back-to-back single-pass encodes on one stream and workspace need one reset before the
+ * first only; the error flags stay until blt_bpe_check_workspace or a reset. */
 int blt_bpe_encode_device_ex(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
                              uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
                              void *stream, uint64_t *out_tokens, uint32_t flags);

@@ -338,6 +338,39 @@ def test_device_api_chunk_offsets():
     assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp)
 
 
+@pytest.mark.parametrize("cs", [1000, 4096, 1 << 20])
+def test_device_api_self_reset(cs):
+    """Single-pass encodes back to back with BLT_ENCODE_WORKSPACE_ZEROED after one reset, sizes
+    growing and shrinking on one workspace: the kernel's last workgroup zeroes the ticket and the
+    status words again (the byte-scan kernel at chunk sizes >= 4096, the generic byte pass below),
+    so each launch gives the oracle's tokens and leaves the control block and status words zero."""
+    import torch
+    rng = np.random.default_rng(5)
+    m = {}
+    while len(m) < 300:
+        m[(int(rng.integers(97, 123)), int(rng.integers(97, 123)))] = 256 + len(m)
+    s = blt_amd.BpeStrategy(m)
+    sizes = [(5 << 20) + 3, 1 << 20, 77777, (5 << 20) + 3, 1, (3 << 20) + 1]
+    nmax = max(sizes)
+    data = np.frombuffer(bytes(rng.integers(97, 123, nmax, dtype=np.uint8)), np.uint8)
+    d_in = torch.from_numpy(data.copy()).cuda()
+    d_out = torch.empty(2 * nmax, dtype=torch.uint8, device="cuda")
+    ws_b = s.workspace_size(nmax, cs)
+    ws = torch.full((ws_b,), 0xA5, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    s.workspace_reset(ws.data_ptr(), nmax, cs, stream)
+    oracle = O.COracle(m)
+    for n in sizes:
+        d_out.zero_()
+        s.encode_device_prezeroed(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), ws_b, stream)
+        torch.cuda.synchronize()
+        exp = oracle.run(data[:n], cs, threads=8)
+        assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), n
+        zero_region = 64 + 8 * ((n + 32767) // 32768)
+        assert not ws[:zero_region].any().item(), n
+    s.check_workspace(ws.data_ptr(), stream)
+
+
 @pytest.mark.parametrize("cs", [4095, 4096, 4097, 6000, 8191, 32768, 32769, 65536 + 7])
 @pytest.mark.parametrize("kind", ["run", "random"])
 def test_columnar_chunk_edges(cs, kind):
