@@ -174,13 +174,19 @@ __device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint
 // Self-reset of a single-pass launch: the last workgroup to leave zeroes the ticket and the
 // status words (every look-back is over by then), so the next launch on this workspace needs no
 // memset (BLT_ENCODE_WORKSPACE_ZEROED).  The error flags and first-error record stay.  Each
-// thread's stores are complete before its workgroup counts itself out, so a late status publish
-// cannot land after the zeroing.  flag: a workgroup-shared word the caller is done with.
+// wave's stores are acknowledged (vmcnt(0): the status publishes are agent-scope atomics, acked at
+// the coherence point) before its workgroup counts itself out, so a late publish cannot land after
+// the zeroing; the zeroing itself reaches the next launch through the kernel-end writeback.  (An
+// agent-scope fence here writes back and invalidates the XCD's L2 under the workgroups still
+// running: measured, the kernel 75 us slower.)  flag: a workgroup-shared word the caller is done with.
 __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles, uint32_t* flag) {
-    __threadfence();
+#ifdef BLT_NO_SELF_RESET   // experiment builds (tools/build_variant.sh): the kernel as before
+    return;
+#endif
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     __syncthreads();
     if (threadIdx.x == 0)
-        *flag = __hip_atomic_fetch_add(p.ctl + kCtlLeft, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+        *flag = __hip_atomic_fetch_add(p.ctl + kCtlLeft, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
     __syncthreads();
     if (*flag) {
         uint4* st = reinterpret_cast<uint4*>(p.status);   // 16-byte aligned (after the control block)
