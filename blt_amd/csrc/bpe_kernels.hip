@@ -721,7 +721,10 @@ constexpr int kGroups = kS * kWaves;
 // 761 (2-byte aligned start + up to 1522 bytes), all the LDS the table leaves: every range of text
 // or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
 // in two parts of 32 lanes (at most 512 tokens each).
-constexpr int kStageWave = 1536 * (16 / kWaves);    // the LDS the table leaves, shared by the waves
+#ifndef BLT_STAGE_WAVE
+#define BLT_STAGE_WAVE (1536 * (16 / BLT_WAVES))
+#endif
+constexpr int kStageWave = BLT_STAGE_WAVE;    // the LDS the table leaves, shared by the waves
 // Look-back windows of 64 status words per round trip.  (Measured: 2 or 4 windows cost more
 // through register spills than the extra round trips they save.)
 constexpr int kLbWin = 1;
@@ -788,7 +791,7 @@ using TileState = TileStateT<kS>;
 // ---- per-tile scalars ---------------------------------------------------------------------
 struct TInfo {
     uint32_t rn;    // positions left in the buffer from the tile start (clamped to 2^31 - 1)
-    uint32_t bge;   // first chunk start >= the tile start, relative (clamped to 2^16)
+    uint32_t bge;   // first chunk start >= the tile start, relative (clamped to kFarPos)
     uint64_t k0;    // its chunk index
 };
 
@@ -796,6 +799,9 @@ struct TInfo {
 // When the chunk size is a whole number of tiles (every chunk size of the configs: 16 MiB = 512
 // tiles), T / (cs / tile) by a 32-bit high multiply with the host's reciprocal and at most two
 // corrections; otherwise tile0 / cs by a 64-bit high multiply.
+// "No chunk start in this tile or the first wave range after it": two tiles from the tile start
+// (chunk starts and chunk sizes are capped there, so a range's one-past-the-end test never fires).
+constexpr uint32_t kFarPos = 2u * (uint32_t)kTilePosBytes;
 __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
     TInfo t;
     const uint64_t tile0 = (uint64_t)T * kTilePosBytes;
@@ -808,7 +814,7 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
         if (r >= d) { q += 1u; r -= d; }
         if (r >= d) { q += 1u; r -= d; }
         const uint32_t left_tiles = r ? d - r : 0u;   // tiles to the next chunk start
-        t.bge = left_tiles > 2u ? 0x10000u : left_tiles * (uint32_t)kTilePosBytes;
+        t.bge = left_tiles > 2u ? kFarPos : left_tiles * (uint32_t)kTilePosBytes;
         t.k0 = (uint64_t)q + (r ? 1u : 0u);
         return t;
     }
@@ -818,7 +824,7 @@ __device__ __forceinline__ TInfo tile_info(const PassParams& p, uint32_t T) {
     if (r >= cs) { q += 1; r -= cs; }
     if (r >= cs) { q += 1; r -= cs; }
     const uint64_t d = r ? cs - r : 0;
-    t.bge = (uint32_t)(d > 0x10000ull ? 0x10000ull : d);
+    t.bge = (uint32_t)(d > kFarPos ? kFarPos : d);
     t.k0 = q + (r ? 1u : 0u);
     return t;
 }
@@ -1012,18 +1018,27 @@ __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, in
     const uint32_t hb = below != 0;
     const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
     const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
-    // a tile has at most 32768 tokens per hypothesis: both fit one packed scan
-    const uint32_t my = (cin0 ? g1 : g0) | ((cin1 ? g1 : g0) << 16);
-    const uint32_t inc = wave_scan(my);
-    const uint32_t exc = inc - my;
+    uint32_t exc0, exc1, tot0, tot1;
+    if constexpr ((uint64_t)NG * kWavePos < 65536u) {
+        // a tile has at most 32768 tokens per hypothesis: both fit one packed scan
+        const uint32_t my = (cin0 ? g1 : g0) | ((cin1 ? g1 : g0) << 16);
+        const uint32_t inc = wave_scan(my);
+        const uint32_t exc = inc - my;
+        exc0 = exc & 0xFFFFu; exc1 = exc >> 16;
+        const uint32_t tot = lane_u32(inc, 63);
+        tot0 = tot & 0xFFFFu; tot1 = tot >> 16;
+    } else {   // 64 KiB tiles: up to 65536 tokens, one scan per hypothesis
+        const uint32_t my0 = cin0 ? g1 : g0, my1 = cin1 ? g1 : g0;
+        const uint32_t inc0 = wave_scan(my0), inc1 = wave_scan(my1);
+        exc0 = inc0 - my0; exc1 = inc1 - my1;
+        tot0 = lane_u32(inc0, 63); tot1 = lane_u32(inc1, 63);
+    }
     if (lane < NG) {
         gin[lane][0] = cin0;
         gin[lane][1] = cin1;
-        gin[lane][2] = exc & 0xFFFFu;
-        gin[lane][3] = exc >> 16;
+        gin[lane][2] = exc0;
+        gin[lane][3] = exc1;
     }
-    const uint32_t tot = lane_u32(inc, 63);
-    const uint32_t tot0 = tot & 0xFFFFu, tot1 = tot >> 16;
     const uint32_t tident = nonid == 0;
     const uint32_t tcout = nonid ? (uint32_t)((cmask >> (63 - __clzll(nonid))) & 1ull) : 0u;
     const uint32_t co0 = tident ? 0u : tcout, co1 = tident ? 1u : tcout;
@@ -1541,7 +1556,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t wave = uni((uint32_t)tid >> 6);
     const uint64_t n = p.n;
     const uint32_t ntiles = p.ntiles;
-    const uint32_t cs32 = (uint32_t)(p.cs > 0x10000ull ? 0x10000ull : p.cs);
+    const uint32_t cs32 = (uint32_t)(p.cs > kFarPos ? kFarPos : p.cs);
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
     const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
