@@ -1563,13 +1563,11 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
     if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
-    // The first two tiles are static, b and b + grid (not consecutive: two consecutive tiles in
-    // one workgroup serialise, measured); later ones are claimed from the counter past 2 grid.
-    // (Claiming the first two with atomics put 512 contended round trips ahead of the first
-    // load: cfg2 0.0868 -> 0.0845 ms without them, cfg3 unchanged; profiles/r03_static_tickets_ab.txt.)
+    // the tickets first: a claim waits for its atomic, and the next one is claimed a round trip
+    // later (other workgroups' claims in between: measured, two consecutive tiles are slower)
     if (tid == 0) {
-        s_tk[kRing - 2] = blockIdx.x;                // T
-        s_tk[kRing - 1] = blockIdx.x + gridDim.x;    // Tq, the tile after it
+        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);   // T
+        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);   // Tq, the tile after it
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
@@ -1623,7 +1621,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         // order stays close to publish order (a tile claimed further ahead lands behind
         // later-claimed ones and stalls their look-backs)
         uint32_t tk = kNone;
-        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u) + 2u * gridDim.x;
+        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
         // ---- phase 1 of T; the last wave to finish it resolves and publishes T ----------------
@@ -2260,7 +2258,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     const bool has_coff = p.chunk_off != nullptr;
     const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
     // the grid was sized for the token bound; workgroups past the tiles the previous pass left leave
-    // before copying the table (the ones below take every tile: b, b + grid, then the counter)
+    // before copying the table (the ones below claim every ticket)
     if (blockIdx.x >= ntiles) return;
     // tokens from sub-tile j's wave range start of tile T to the buffer end (clamped)
     auto rem_of = [&](uint32_t T, int j) {
@@ -2285,8 +2283,8 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
         }
     }
     if (tid == 0) {
-        s_tk[kRing - 2] = blockIdx.x;                // the first two tiles static (as the byte pass)
-        s_tk[kRing - 1] = blockIdx.x + gridDim.x;
+        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);
+        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
@@ -2331,7 +2329,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
         }
         uint32_t tk = kNone;
-        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u) + 2u * gridDim.x;
+        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
         asm volatile("" ::: "memory");
 
         bool lbw = wave == 0;
