@@ -334,6 +334,12 @@ template <> struct Seg<uint16_t> {
     static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
 };
 
+// u16 passes of merge_pass_body: chunk starts from an LDS list per tile (experiment switch: 0 walks
+// p.cstart from global memory as before)
+#ifndef BLT_BND_LDS
+#define BLT_BND_LDS 1
+#endif
+
 // Global -> LDS copy of n 16-byte units by nthr threads, kBatch loads in flight per thread
 // before their stores (a rolled loop waits for every load: one L2/MALL round trip each).
 template <int kBatch, typename T>
@@ -386,6 +392,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     __shared__ uint32_t s_ticket;
     __shared__ uint32_t s_C;
     __shared__ uint64_t s_O;
+    // u16 passes: the tile's chunk starts (token positions from p.cstart), relative to the tile's
+    // first position, 0xFFFF past the last; fetched in one parallel round per tile
+    __shared__ uint16_t s_bnd[kDense ? 1 : kThreads];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -418,6 +427,37 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         const uint32_t T = s_ticket;
         if (T >= p.ntiles) break;
         const uint64_t tile0 = (uint64_t)T * kTileT;
+        // Chunk starts of a u16 pass (p.cs == 0: p.cstart holds them, token positions): the
+        // tile's first kThreads of them go to LDS in one round of parallel loads, and each lane
+        // searches that list for its own 16 positions, instead of walking p.cstart one dependent
+        // global load per chunk start, per sub-tile and twice per tile (measured on the f2 chain
+        // row's tail passes, 16 chunks of a few hundred tokens: 22.6 -> 17.6 us per launch, the
+        // row 0.86 -> 0.83 ms).  nb = kThreads: the list may be incomplete, and the tile walks
+        // p.cstart as before.
+        uint32_t nb = kThreads;
+        uint64_t bk0 = 0;
+        if constexpr (!kDense && BLT_BND_LDS) {
+            if (p.cs == 0) {
+                (void)first_boundary(p, tile0, bk0);   // uniform: the same loads on every lane
+                const uint64_t k = bk0 + (uint64_t)tid;
+                uint32_t rel = 0xFFFFu;
+                if (k < p.nchunks) {
+                    const uint64_t b = p.cstart[k];
+                    if (b < p.n && b <= tile0 + kTileT) rel = (uint32_t)(b - tile0);   // <= 32768
+                }
+                s_bnd[tid] = (uint16_t)rel;
+                nb = (uint32_t)__syncthreads_count(rel != 0xFFFFu);   // chunk starts are increasing
+            }
+        }
+        // first entry of s_bnd[0 .. nb) that is >= lo
+        auto bnd_lower = [&](uint32_t lo) {
+            uint32_t a = 0, z = nb;
+            while (a < z) {
+                const uint32_t mid = (a + z) >> 1;
+                if (s_bnd[mid] < lo) a = mid + 1; else z = mid;
+            }
+            return a;
+        };
 
         Seg<InT> seg[kSubT];
         uint32_t vals[kSubT][8];
@@ -458,7 +498,14 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
             const uint32_t vmask = pos >= p.n ? 0u : (p.n - pos >= 16 ? 0xFFFFu : ((1u << (uint32_t)(p.n - pos)) - 1u));
             m &= (vmask >> 1) | (pos + 16 < p.n ? 0x8000u : 0u);
             // no merge across a chunk end: clear m at b - 1 for chunk starts b in (sub0, sub0 + kSubPos]
-            {
+            if (nb < (uint32_t)kThreads) {   // (uniform) this lane's chunk starts b in [pos + 1, pos + 16]
+                const uint32_t lo = (uint32_t)(pos - tile0) + 1u;
+                for (uint32_t a = bnd_lower(lo); a < nb; ++a) {
+                    const uint32_t r = s_bnd[a];
+                    if (r > lo + 15u) break;
+                    m &= ~(1u << (r - lo));
+                }
+            } else {
                 uint64_t kidx;
                 uint64_t b = first_boundary(p, sub0 + 1 < p.n ? sub0 + 1 : p.n, kidx);
                 while (b < p.n && b <= sub0 + kSubPos) {
@@ -567,7 +614,15 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
                 }
             }
             // token offsets of chunk starts in this segment
-            if (p.chunk_off) {
+            if (p.chunk_off && nb < (uint32_t)kThreads) {   // this lane's chunk starts in [pos, pos + 16)
+                const uint32_t lo = (uint32_t)(pos - tile0);
+                for (uint32_t a = bnd_lower(lo); a < nb; ++a) {
+                    const uint32_t r = s_bnd[a];
+                    if (r > lo + 15u) break;
+                    const uint32_t before = __popc(L & ((1u << (r - lo)) - 1u));
+                    p.chunk_off[bk0 + a] = O + lane_off + before;
+                }
+            } else if (p.chunk_off) {
                 uint64_t kidx;
                 uint64_t b = first_boundary(p, sub0 < p.n ? sub0 : p.n, kidx);
                 while (b < p.n && b < sub0 + kSubPos) {
