@@ -146,6 +146,23 @@ def test_wrapping_merges_file(tmp_path, kind):
         assert np.array_equal(lens, elens)
 
 
+@pytest.mark.parametrize("cs", [37, 64, 256, 300, 1000, 2047])
+def test_u16_passes_many_chunk_starts_per_tile(cs):
+    """u16 passes over chunks of a few to a few hundred tokens (merge_tokens_kernel,
+    tokenizer.rs:63-86 per chunk): a 32K-position tile holds tens to over a thousand chunk starts,
+    so both the tile's LDS chunk-start list (fewer starts than threads) and its walk of the
+    global list run; cs 64 and 256 on runs of 'a' put chunk starts exactly on tile edges."""
+    text = synth.text(4 * TILE + 333, seed=7)
+    runs = np.full(4 * TILE + 333, 97, np.uint8)
+    for m, data in ((synth.CHAINED_TEXT_MAP, text), (synth.doubling_chain(6), runs), ({(97, 97): 97}, runs)):
+        s = blt_amd.BpeStrategy(m)
+        assert s.info()[1] is False
+        got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+        exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+        assert np.array_equal(got, exp), (cs, m)
+        assert np.array_equal(lens, elens), (cs, m)
+
+
 def test_chained_map_long():
     m = {(97, 97): 97}  # "aa" -> "a": log2(n) passes
     data = b"a" * 100000 + b"b" + b"a" * 3
