@@ -166,7 +166,38 @@ def extra_configs(blt_amd, synth, O, threads, only=()):
         if only and name not in only:
             continue
         res[name] = general_map_rate(blt_amd, synth, O, threads, name)
+    if not only or "basic" in only:
+        res["basic"] = basic_rate(blt_amd, synth, O, threads)
     return res
+
+
+def basic_rate(blt_amd, synth, O, threads, n=GIB, reps=20, warmup=5):
+    """Row f3 / cfg1 at scale: the basic strategy (tokenizer.rs:108-124, byte b -> BE [0, b]) on
+    1 GiB of seeded random bytes (cfg1's generator, seed 1), basic_expand_kernel device-resident,
+    median of HIP-event timings; algorithmic bytes N + 2N; checked against the oracle."""
+    import torch
+    host = synth.random_bytes(n, seed=1)
+    s = blt_amd.BasicTokenizationStrategy()
+    d_in = torch.from_numpy(host).cuda()
+    d_out = torch.empty(2 * n, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    for _ in range(warmup):
+        s.encode_device(d_in.data_ptr(), n, d_out.data_ptr(), sp)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        s.encode_device(d_in.data_ptr(), n, d_out.data_ptr(), sp)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+    got = d_out.cpu().numpy()
+    exp = O.COracle(None).run(host, CHUNK, threads=threads)
+    algo = 3 * n
+    return {"workload": "cfg1 at scale: 1024 MiB seeded random bytes, basic strategy (no merges)", "bytes": n,
+            "kernel": "basic_expand_kernel", "kernel_ms": round(ms, 4), "input_GBps": round(n / ms / 1e6, 1),
+            "achieved_GBps": round(algo / ms / 1e6, 1), "frac": round(algo / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
 
 
 def general_workload(synth, name):
@@ -478,13 +509,16 @@ def main():
     usable, affinity, ncpu = usable_cores()
     threads = max(1, args.cpu_threads or usable)
     extras = {}
-    if rank == 0 and not args.no_cpu_baseline and distributed:
-        # N > 1: the CPU baseline is reported at N = 1 only; rank 0 still checks its shard
-        # bit-exact, with the dense single-pass oracle (outside the timed region)
+    if distributed and not args.no_cpu_baseline:
+        # N > 1: the CPU baseline is reported at N = 1 only; EVERY rank checks its own shard
+        # bit-exact against the C oracle (outside the timed region, the host cores split between
+        # the ranks), and the flags are ANDed over the ranks (an all_reduce MIN of 0/1)
         from oracle import oracle as O
-        fast = O.fast_run(merges, host, CHUNK, threads=threads)
-        if fast is not None:
-            exact = bool(np.array_equal(fast, d_out[:2 * tokens].cpu().numpy()))
+        exp = O.COracle(merges).run(host, CHUNK, threads=max(1, threads // world))
+        got = d_out[:2 * tokens].cpu().numpy()
+        mine = bool(exp.size == got.size and np.array_equal(exp, got))
+        del exp, got
+        exact = shard.all_ranks_true(mine, device="cuda" if backend == "nccl" else None)
     elif rank == 0 and not args.no_cpu_baseline:
         from oracle import oracle as O
         orc = O.COracle(merges)

@@ -209,8 +209,10 @@ class BpeStrategy(TokenizationStrategy):
     def encode_device_prezeroed(self, d_in: int, n: int, chunk_size: int, d_out: int, d_workspace: int,
                                 workspace_bytes: int, stream: int = 0, d_chunk_off: int = 0) -> None:
         """Enqueues only the merge-scan kernel.  The workspace's look-back words must be zero: a
-        workspace_reset on the stream since the last encode, or a single-pass encode last (its
-        kernel leaves them zeroed)."""
+        workspace_reset for an n at least this one on the stream since the last encode, or
+        single-pass encodes last (each kernel leaves its words zeroed).  A launch over more tiles
+        than the workspace is known zeroed for refuses (writes nothing, error bit 32: the next
+        check_workspace raises and the handle's next call fails until clear_error)."""
         _lib.check(self._L.blt_bpe_encode_device_ex(self._h, d_in, n, chunk_size, d_out, d_chunk_off or None,
                                                     d_workspace, workspace_bytes, stream or None, None, 1))
 

@@ -612,7 +612,8 @@ int ctl_error(const uint32_t* ctl) {
     if (ctl[1])
         return fail(BLT_E_IO,
                     "merge-scan device check failed (flags 0x%x: 1 look-back timeout, 2 output range, 4 prefix "
-                    "invariant, 8 workgroup wait timeout, 16 chunk map; first at tile %u sub-tile %u, O=%llu, "
+                    "invariant, 8 workgroup wait timeout, 16 chunk map, 32 workspace not zeroed for this size "
+                    "(BLT_ENCODE_WORKSPACE_ZEROED past the last reset); first at tile %u sub-tile %u, O=%llu, "
                     "value=%llu, C=%u)",
                     ctl[1], ctl[2] ? ctl[2] - 1 : 0, ctl[3], (unsigned long long)ctl[4] | ((unsigned long long)ctl[5] << 32),
                     (unsigned long long)ctl[6] | ((unsigned long long)ctl[7] << 32), ctl[8]);
@@ -683,6 +684,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.debug = g_debug_tiles;
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
+    p.ws_check = (ws_zeroed && !in_u16 && !chain) ? 1u : 0u;   // the caller's BLT_ENCODE_WORKSPACE_ZEROED
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, h->byte_mode, (chain && h->live_first) ? 1 : 0, dev, s));
     else if (in_u16 && tok_scan) HIP_TRY(blt::launch_scan_tokens(p, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
@@ -725,8 +727,10 @@ int run_fused(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint
 }
 
 // A device error flagged during a general map's chain: the sticky message, with the control
-// block's flags and first-error record of the chain's u16 scan passes (their chunk-map kernel
-// resets only the ticket).
+// block's flags and first-error record when they survive.  The u16 scan passes keep them (their
+// chunk-map kernel resets only the ticket); a generic u16 pass (merge_tokens_kernel, chunks under
+// kTokRange tokens) zeroes the whole control block before its launch, so an error flagged earlier in
+// the chain is reported by the sticky message alone.
 int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t passes) {
     if (!sticky_check(h)) return 0;
     const std::string sticky_msg = t_err;
@@ -1437,6 +1441,10 @@ int blt_bpe_workspace_reset(const blt_bpe* h, void* d_ws, uint64_t n, uint64_t c
     if (!h || !d_ws || cs == 0) return fail(BLT_E_INVALID_INPUT, "bad argument");
     const WsLayout L = ws_layout(h->single_pass, n, cs);
     HIP_TRY(hipMemsetAsync(d_ws, 0, L.zero_bytes, (hipStream_t)stream));
+    // the status words a BLT_ENCODE_WORKSPACE_ZEROED launch may rely on (it refuses beyond them)
+    if (L.ntiles <= 0xFFFFFFFFull)
+        HIP_TRY(hipMemsetD32Async(static_cast<uint32_t*>(d_ws) + blt::kCtlCover, (int)(uint32_t)L.ntiles, 1,
+                                  (hipStream_t)stream));
     return 0;
 }
 

@@ -17,6 +17,9 @@ constexpr uint64_t kTilePosBytes = BLT_TILE_BYTES;   // positions per look-back 
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 constexpr uint32_t kCtlLeft = 15;             // ctl word: workgroups of a single-pass launch that have left
+constexpr uint32_t kCtlCover = 14;            // ctl word: status words [0, ctl[14]) are known zero (set by
+                                              // blt_bpe_workspace_reset and by a single-pass launch's self-reset);
+                                              // a launch told its workspace is zeroed checks its tiles against it
 
 // Parameters of one merge pass over a whole buffer of positions.
 struct PassParams {
@@ -61,6 +64,8 @@ struct PassParams {
                                // marks a merge valued its own first byte
     uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
                                // error bits in ctl[1], so the handle's next call fails
+    uint32_t ws_check;         // single-pass byte kernels launched without a memset (BLT_ENCODE_WORKSPACE_ZEROED):
+                               // refuse (error bit 32, no output) when ntiles > ctl[kCtlCover]
     uint32_t* fused_fail;      // fused passes 1 + 2: set to 1 when a wave range's halo holds no
                                // restart (the host then runs the two-kernel chain instead)
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,

@@ -192,8 +192,24 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
         uint4* st = reinterpret_cast<uint4*>(p.status);   // 16-byte aligned (after the control block)
         const uint32_t units = (ntiles + 1u) / 2u;         // within the zeroed region (rounded to 16 bytes)
         for (uint32_t i = threadIdx.x; i < units; i += blockDim.x) st[i] = make_uint4(0u, 0u, 0u, 0u);
-        if (threadIdx.x == 0) { p.ctl[0] = 0u; p.ctl[kCtlLeft] = 0u; }
+        if (threadIdx.x == 0) {
+            p.ctl[0] = 0u;
+            p.ctl[kCtlLeft] = 0u;
+            // words [0, ntiles) are zero now, and the ones past them were before (untouched here)
+            if (ntiles > p.ctl[kCtlCover]) p.ctl[kCtlCover] = ntiles;
+        }
     }
+}
+
+// A launch told its workspace is zeroed (p.ws_check) whose tiles reach past the status words known
+// zero refuses: error bit 32 (one workgroup flags it), no ticket, no output, no self-reset.  Uniform
+// per launch (every workgroup reads the same word, written before the launch on its stream).
+__device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles) {
+    if (!p.ws_check) return false;
+    const uint32_t cover = __hip_atomic_load(p.ctl + kCtlCover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ntiles <= cover) return false;
+    if (blockIdx.x == 0 && threadIdx.x == 0) flag_error(p.ctl, KARG(sticky), 32u);
+    return true;
 }
 
 // Lane i's 64-bit value from its two halves.  readlane returns int: cast each half to uint32_t
@@ -395,6 +411,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     // u16 passes: the tile's chunk starts (token positions from p.cstart), relative to the tile's
     // first position, 0xFFFF past the last; fetched in one parallel round per tile
     __shared__ uint16_t s_bnd[kDense ? 1 : kThreads];
+    // a start on the next tile's first position is stored as kTileT itself: it must stay below the
+    // 0xFFFF end marker (a 64K-position tile would wrap it to 0, a start at the tile's first position)
+    static_assert(kTileT < 0xFFFFu, "s_bnd: tile-relative u16 chunk starts");
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -409,6 +428,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         // the grid was sized for the input's bound; workgroups past the tiles there are leave
         // before copying the table (the ones below claim every ticket)
         if (blockIdx.x >= p.ntiles) return;
+    }
+    if constexpr (kDense) {
+        if (ws_refused(p, p.ntiles)) return;
     }
     const InT* in = reinterpret_cast<const InT*>(p.in);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
@@ -1615,6 +1637,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
     const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
+    if (ws_refused(p, ntiles)) return;
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
     if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
@@ -1862,7 +1885,7 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     const uint64_t n = token_count(p);
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
-    if (r == 0) p.ctl[0] = 0u;
+    if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
     const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
     if (lo >= n) return;
     const uint64_t* cs = p.cstart;

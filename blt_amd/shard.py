@@ -51,6 +51,16 @@ def max_over_ranks(values: Sequence[float], device=None) -> List[float]:
     return [float(v) for v in t.cpu()]
 
 
+def all_ranks_true(flag: bool, device=None) -> bool:
+    """AND of a per-rank flag over every rank (the flag itself without a process group)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
 def gather_ranges(rng: Tuple[int, int], device=None) -> List[Tuple[int, int]]:
     """Every rank's (b0, b1), in rank order (this rank's alone without a process group)."""
     import torch

@@ -175,15 +175,21 @@ int blt_bpe_encode_device(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uin
 
 /* Flags of blt_bpe_encode_device_ex. */
 #define BLT_ENCODE_WORKSPACE_ZEROED 1u /* the workspace's look-back words are zero: the caller ran
-                                          blt_bpe_workspace_reset on this stream since the last encode,
-                                          or the last encode on it was a single-pass one (single-pass
-                                          maps; ignored otherwise) */
+                                          blt_bpe_workspace_reset on this stream for an n at least this
+                                          call's since the last encode, or the last encodes on it were
+                                          single-pass ones (single-pass maps; ignored otherwise) */
 
 /* As blt_bpe_encode_device, with flags.  With BLT_ENCODE_WORKSPACE_ZEROED the call enqueues only
  * the merge-scan kernel, so events around it time that kernel alone.  A single-pass encode leaves
  * the workspace's ticket and status words zeroed when its kernel ends (its last workgroup resets
  * them), so back-to-back single-pass encodes on one stream and workspace need one reset before the
- * first only; the error flags stay until blt_bpe_check_workspace or a reset. */
+ * first only; the error flags stay until blt_bpe_check_workspace or a reset.  The control block
+ * records how many status words are known zero (word 14: set by blt_bpe_workspace_reset to its
+ * n's tile count, raised by each single-pass kernel's self-reset to its own, cleared by a general
+ * map's passes and by blt_bpe_check_workspace after an error).  A flagged launch needing more
+ * words than that refuses: it writes nothing and flags error bit 32, which the next
+ * blt_bpe_check_workspace reports and which fails the handle's next call (BLT_E_IO) until
+ * blt_bpe_clear_error.  Reset for the largest n encoded with the flag. */
 int blt_bpe_encode_device_ex(const blt_bpe *h, const uint8_t *d_in, uint64_t n, uint64_t chunk_size,
                              uint8_t *d_out, uint64_t *d_chunk_off, void *d_workspace, size_t workspace_bytes,
                              void *stream, uint64_t *out_tokens, uint32_t flags);

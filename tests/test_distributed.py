@@ -38,8 +38,10 @@ def _worker(rank, world, port, data, merges, chunk_size, q):
         mx = shard.max_over_ranks([float(rank + 1), float(10 - rank)])
         # bench.py's config.rank_bytes: every rank's range of cfg4's 8 GiB stream
         rg = shard.gather_ranges(shard.rank_bytes(8 << 30, 16 << 20, rank, world))
+        # bench.py's per-rank bit-exact flags, ANDed over the ranks: all true, and one rank false
+        ok = (shard.all_ranks_true(True), shard.all_ranks_true(rank != world - 1))
         q.put((rank, local.size, None if full is None else full.tobytes(),
-               None if full_lens is None else full_lens.tolist(), mx, rg))
+               None if full_lens is None else full_lens.tolist(), mx, rg, ok))
     finally:
         dist.destroy_process_group()
 
@@ -76,6 +78,8 @@ def test_two_rank_stitch_matches_single_process(chunk_size):
     # every rank sees every rank's byte range, in rank order
     exp_rg = [shard.rank_bytes(8 << 30, 16 << 20, r, 2) for r in range(2)]
     assert res[0][5] == exp_rg and res[1][5] == exp_rg == [(0, 4 << 30), (4 << 30, 8 << 30)]
+    # a shard that fails its check fails the run on every rank
+    assert res[0][6] == res[1][6] == (True, False)
 
 
 def test_partition_matches_host_library():

@@ -5,6 +5,8 @@
   per-chunk token counts checked against the size-independent bounds (n/2 <= M <= n per chunk,
   offsets monotone, last offset = total).
 - f2: 3 GiB of text through a chained general map (u16 passes past 2^31 token bytes).
+- cfg2: BASELINE's exact workload (100 MiB of seed-2 text, the 256 merges ranked from it, 16 MiB
+  chunks = 7 chunks, the last one partial), stream and per-chunk offsets bit-exact.
 - cfg4: 8 GiB of text cut into the 8 contiguous chunk ranges of an 8-GPU run (blt_amd.shard,
   the partition bench.py and blt_bpe_process_chunks use); every shard runs as its own launch
   and the rank-order stitch equals the one-shot oracle stream: sharding is exact.
@@ -55,6 +57,20 @@ def test_cfg5_random_bytes_4gib():
     sizes = np.diff(np.minimum(np.arange(off.size, dtype=np.int64) * CHUNK, n))
     assert off[0] == 0 and off[-1] == got.size // 2
     assert np.all(lens * 2 >= sizes) and np.all(lens <= sizes)
+
+
+def test_cfg2_text_100mib_256_merges():
+    """cfg2 exactly as bench.py builds it (bench.workload): 100 MiB of seed-2 text, the top-256
+    adjacent pairs of that text as merges, --chunksize 16MB (6 whole chunks and a 4 MiB tail)."""
+    n = 100 << 20
+    data = synth.text(n, seed=2)
+    m = synth.merges_dict(synth.top_pair_merges(data, 256))
+    assert len(m) == 256
+    got, off = _device_encode(blt_amd.BpeStrategy(m), data, CHUNK)
+    exp, elens = O.COracle(m).run(data, CHUNK, threads=16, return_lens=True)
+    assert elens.size == 7
+    assert np.array_equal(got, exp)
+    assert np.array_equal(np.diff(off) * 2, elens)
 
 
 def test_cfg4_eight_shards_8gib():

@@ -384,8 +384,55 @@ def test_device_api_self_reset(cs):
         exp = oracle.run(data[:n], cs, threads=8)
         assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), n
         zero_region = 64 + 8 * ((n + 32767) // 32768)
-        assert not ws[:zero_region].any().item(), n
+        # every word zero but ctl[14], the count of status words known zero (the reset's nmax tiles)
+        w = ws[:zero_region].clone()
+        assert w[56:60].cpu().numpy().view(np.uint32)[0] == (nmax + 32767) // 32768, n
+        w[56:60] = 0
+        assert not w.any().item(), n
     s.check_workspace(ws.data_ptr(), stream)
+
+
+@pytest.mark.parametrize("cs", [4096, 1 << 20, 1000])
+def test_zeroed_flag_refuses_past_reset(cs):
+    """BLT_ENCODE_WORKSPACE_ZEROED after a reset for a smaller n.  The reset records how
+    many status words it zeroed (ctl[14]); a flagged launch over more tiles refuses (error bit 32,
+    the handle's sticky error, no output) instead of reading stale look-back words.  A reset for the
+    larger n, or a launch without the flag (which zeroes for itself), then runs bit-exact."""
+    import torch
+    rng = np.random.default_rng(cs)
+    m = {(int(a), int(b)): 256 + i for i, (a, b) in enumerate(rng.integers(97, 123, (200, 2)))}
+    s = blt_amd.BpeStrategy(m)
+    small, large = 3 * 32768 + 5, 40 * 32768 + 11
+    data = rng.integers(97, 123, large, dtype=np.uint8)
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.zeros(2 * large, dtype=torch.uint8, device="cuda")
+    wsb = s.workspace_size(large, cs)
+    ws = torch.full((wsb,), 0xA5, dtype=torch.uint8, device="cuda")   # stale words past the small reset
+    st = torch.cuda.current_stream().cuda_stream
+    oracle = O.COracle(m)
+    s.workspace_reset(ws.data_ptr(), small, cs, st)
+    s.encode_device_prezeroed(d_in.data_ptr(), small, cs, d_out.data_ptr(), ws.data_ptr(), wsb, st)
+    torch.cuda.synchronize()
+    exp = oracle.run(data[:small], cs, threads=8)
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    d_out.zero_()
+    s.encode_device_prezeroed(d_in.data_ptr(), large, cs, d_out.data_ptr(), ws.data_ptr(), wsb, st)
+    torch.cuda.synchronize()
+    assert not d_out.any().item()   # refused: nothing written
+    with pytest.raises(blt_amd.BltError):
+        s.check_workspace(ws.data_ptr(), st)   # error bit 32 (and it clears the control block)
+    assert s.clear_error()                     # the handle's sticky error was set
+    s.workspace_reset(ws.data_ptr(), large, cs, st)
+    s.encode_device_prezeroed(d_in.data_ptr(), large, cs, d_out.data_ptr(), ws.data_ptr(), wsb, st)
+    torch.cuda.synchronize()
+    exp = oracle.run(data, cs, threads=8)
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    s.check_workspace(ws.data_ptr(), st)
+    # a launch without the flag zeroes its own words, whatever the last reset covered
+    s.workspace_reset(ws.data_ptr(), small, cs, st)
+    tok = s.encode_device(d_in.data_ptr(), large, cs, d_out.data_ptr(), ws.data_ptr(), wsb, st)
+    assert tok == exp.size // 2
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
 
 
 @pytest.mark.parametrize("cs", [4095, 4096, 4097, 6000, 8191, 32768, 32769, 65536 + 7])

@@ -58,7 +58,7 @@ def run_group(outdir, name, counters, bench_args, kernel, script="bench.py"):
                 cname = row["Counter_Name"]
                 sums[cname] = sums.get(cname, 0.0) + float(row["Counter_Value"])
                 disp.setdefault(cname, set()).add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))
-    return {k: sums[k] / max(1, len(disp[k])) for k in sums}, {k: len(v) for k, v in disp.items()}
+    return {k: sums[k] / max(1, len(disp[k])) for k in sums}, {k: len(v) for k, v in disp.items()}, sums
 
 
 def main():
@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--groups", default=",".join(GROUPS))
     ap.add_argument("--kernel", default="scan_bytes_kernel")
     ap.add_argument("--script", default="bench.py")
+    ap.add_argument("--calls", type=int, default=0,
+                    help="calls the script makes (f2 rows: several kernels per call): also report totals / calls")
     argv = sys.argv[1:]
     extra = []
     if "--" in argv:
@@ -75,13 +77,18 @@ def main():
     a = ap.parse_args(argv)
     bench_args = extra or ["--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--no-extra"]
     os.makedirs(a.outdir, exist_ok=True)
-    result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}}
+    result = {"kernel": a.kernel, "bench_args": bench_args, "per_dispatch": {}, "dispatches": {}, "totals": {}}
     for g in a.groups.split(","):
-        vals, nd = run_group(a.outdir, g, GROUPS[g], bench_args, a.kernel, a.script)
+        vals, nd, tot = run_group(a.outdir, g, GROUPS[g], bench_args, a.kernel, a.script)
         result["per_dispatch"].update(vals)
         result["dispatches"].update(nd)
+        result["totals"].update(tot)
+    if a.calls and "FETCH_SIZE" in result["totals"] and "WRITE_SIZE" in result["totals"]:
+        t = result["totals"]
+        result["calls"] = a.calls
+        result["hbm_bytes_per_call"] = int((2.0 * t["FETCH_SIZE"] + t["WRITE_SIZE"]) * 1024 / a.calls)
     pd = result["per_dispatch"]
-    if "FETCH_SIZE" in pd and "WRITE_SIZE" in pd:
+    if "FETCH_SIZE" in pd and "WRITE_SIZE" in pd and a.script == "bench.py":
         result["hbm_bytes_per_launch"] = int((2.0 * pd["FETCH_SIZE"] + pd["WRITE_SIZE"]) * 1024)
         result["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) KiB: gfx950 FETCH_SIZE counts half of wide reads"
         # what bench.py reports as roofline.traffic for the same workload

@@ -1,0 +1,79 @@
+#!/bin/bash
+# One GPU call made of named steps (the maintained runner; round 3's one-off scripts are in
+# tools/history/).  Every GPU step runs under its own time limit and the chain stops at the first
+# failure (set -e), so a fault or a hang ends the call there.
+#
+#   gpurun --timeout 1200 -- 'bash tools/round.sh TAG STEP [STEP ...]'
+#
+# Steps (outputs under gpurun_out/TAG/):
+#   tests              pytest -m gpu (every parity test), tests.log
+#   smoke              __graft_entry__.smoke(), smoke.log
+#   bench              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5, bench.json
+#   bench:ARGS         bench.py with extra arguments (commas for spaces), bench_<n>.json
+#   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/exp/libblt_bpe_LIBTAG.so)
+#   prof:WL            rocprofv3 --kernel-trace --stats of bench.py --workload WL (cfg2|cfg3|cfg5)
+#   proff2[:ROWS]      rocprofv3 kernel stats of the f2 rows (bench.py --only-configs ROWS)
+#   pmc:WL[:GROUPS]    tools/pmc_profile.py on bench.py --workload WL (groups default fetch,write,insts)
+#   pmcf2:ROW[:GROUPS] PMC of one f2 row (tools/f2_row.py: every kernel of its calls, traffic per call)
+#   resources          -Rpass-analysis=kernel-resource-usage of the kernel source (CPU only)
+set -e
+TAG=${1:?tag}
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+nb=0
+for st in "$@"; do
+  IFS=: read -r kind a b <<< "$st"
+  echo "== $st $(date +%T)"
+  case $kind in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 \
+        || { tail -40 "$O/tests.log"; exit 1; }
+      tail -2 "$O/tests.log" ;;
+    smoke)
+      timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      if [ -z "$a" ]; then
+        timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err"
+        python tools/summarize_bench.py "$O/bench.json"
+      else
+        nb=$((nb + 1))
+        timeout -k 10 400 python bench.py ${a//,/ } > "$O/bench_$nb.json" 2> "$O/bench_$nb.err"
+        python tools/summarize_bench.py "$O/bench_$nb.json"
+      fi ;;
+    kbench)
+      lib=""; [ -n "$a" ] && lib="$R/build/exp/libblt_bpe_$a.so"
+      BLT_LIB_PATH=$lib timeout -k 10 300 python tools/kbench.py --check >> "$O/kbench.jsonl" 2> "$O/kbench.err"
+      tail -3 "$O/kbench.jsonl" ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$O/prof_$a" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extra \
+        --workload "$a" > "$O/prof_$a.log" 2>&1)
+      find "$O/prof_$a" -name '*kernel_stats.csv' -exec head -4 {} \; | cut -c1-160 ;;
+    proff2)
+      rows=${a:-multi,wrap,selfval,chain}
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$O/prof_f2" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --only-configs "$rows" \
+        > "$O/prof_f2.log" 2>&1)
+      find "$O/prof_f2" -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-160 ;;
+    pmc)
+      timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --groups "${b:-fetch,write,insts}" -- \
+        --workload "$a" --steps 5 --warmup 2 --no-cpu-baseline --no-extra > "$O/pmc_$a.log" 2>&1
+      tail -3 "$O/pmc_$a.log" ;;
+    pmcf2)
+      # 5 asynchronous calls (tools/f2_row.py): traffic per call = totals / 5
+      timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --kernel "" --script tools/f2_row.py --calls 5 \
+        --groups "${b:-fetch,write}" -- --row "$a" --reps 5 > "$O/pmc_$a.log" 2>&1
+      grep -E "hbm_bytes_per_call|calls" "$O/pmc_$a/pmc_summary.json" ;;
+    resources)
+      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c blt_amd/csrc/bpe_kernels.hip -o /tmp/rk.o \
+        -Rpass-analysis=kernel-resource-usage > "$O/resources.txt" 2>&1
+      grep -E "Function Name|VGPRs:|SGPRs Spill|VGPRs Spill" "$O/resources.txt" | sed 's/.*remark: *//' ;;
+    *)
+      echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
