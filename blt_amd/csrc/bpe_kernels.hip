@@ -55,7 +55,20 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kSeg = 16;                      // positions per lane per sub-tile
 constexpr int kSubPos = kThreads * kSeg;      // 8192 positions per sub-tile
 constexpr int kStageBytes = 2 * kSubPos + 32;
-constexpr uint32_t kSpinLimit = 1u << 20;
+// Spin timeouts are wall-clock time (s_memrealtime, a constant 100 MHz clock), not iteration counts:
+// a predecessor slowed by other work on the device (a co-tenant kernel, another queue's time slice)
+// still finishes well inside them, so only a stuck wait is flagged (a count of
+// sleeps is as long as the clock the waves happen to run at, milliseconds at best).
+constexpr uint32_t kSpinTimeoutTicks = 20000000u;   // 200 ms at 100 MHz
+struct SpinClock {
+    uint32_t t0 = 0;   // low half of the clock (wraps every 43 s; the deltas here are far shorter)
+    // true once the wait has lasted longer than kSpinTimeoutTicks (the first call starts the clock)
+    __device__ __forceinline__ bool expired() {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (t0 == 0) { t0 = t | 1u; return false; }
+        return t - t0 > kSpinTimeoutTicks;
+    }
+};
 static_assert(kTilePos == kSub * kSubPos, "tile geometry");
 
 __device__ __forceinline__ uint32_t swz_index(uint32_t a, uint32_t b) {
@@ -202,11 +215,14 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 }
 
 // A launch told its workspace is zeroed (p.ws_check) whose tiles reach past the status words known
-// zero refuses: error bit 32 (one workgroup flags it), no ticket, no output, no self-reset.  Uniform
-// per launch (every workgroup reads the same word, written before the launch on its stream).
-__device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles) {
-    if (!p.ws_check) return false;
-    const uint32_t cover = __hip_atomic_load(p.ctl + kCtlCover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// zero refuses: error bit 32 (one workgroup flags it) and no output; its workgroups claim no tile
+// but still count themselves out, so the self-reset zeroes its ntiles words as usual.  The word is
+// read at the workgroup's start (a scalar load, written before the launch on its stream) and tested
+// after the table copy, off the critical path.
+__device__ __forceinline__ uint32_t ws_cover(const PassParams& p) {
+    return p.ws_check ? *(const volatile uint32_t*)(p.ctl + kCtlCover) : 0xFFFFFFFFu;
+}
+__device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles, uint32_t cover) {
     if (ntiles <= cover) return false;
     if (blockIdx.x == 0 && threadIdx.x == 0) flag_error(p.ctl, KARG(sticky), 32u);
     return true;
@@ -232,6 +248,7 @@ __device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t&
     Fn64 acc = {0u, 1u, 0ull, 0ull};   // function of tiles (k+1 .. T-1), identity so far
     int64_t k = (int64_t)T - 1;
     uint32_t spins = 0;
+    SpinClock clk;
     for (;;) {
         int64_t idx = k - lane;
         uint64_t s = idx < 0 ? st_incl(1u, 0ull) : st_read(p.status + idx);
@@ -241,7 +258,8 @@ __device__ void lookback(const PassParams& p, uint32_t T, uint32_t& C, uint64_t&
         int f = incl ? (int)__ffsll((unsigned long long)incl) - 1 : 64;
         uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
         if ((ready & need) != need) {
-            if (++spins > kSpinLimit) {   // flagged; the tile writes nothing (C = 2)
+            ++spins;
+            if (clk.expired()) {   // flagged; the tile writes nothing (C = 2)
                 if (lane == 0) flag_error(p.ctl, KARG(sticky), 1u);
                 C = 2u; O = 0ull;
                 return;
@@ -429,9 +447,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         // before copying the table (the ones below claim every ticket)
         if (blockIdx.x >= p.ntiles) return;
     }
-    if constexpr (kDense) {
-        if (ws_refused(p, p.ntiles)) return;
-    }
+    const uint32_t cover = kDense ? ws_cover(p) : 0xFFFFFFFFu;
     const InT* in = reinterpret_cast<const InT*>(p.in);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
 
@@ -443,7 +459,9 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         copy_to_lds<8>(s_hash, p.hbuckets, p.hbytes / 8u, (uint32_t)tid, (uint32_t)kThreads);
     }
 
+    const bool refused = kDense && ws_refused(p, p.ntiles, cover);
     for (;;) {
+        if (refused) break;
         if (tid == 0) s_ticket = atomicAdd(p.ctl, 1u);
         __syncthreads();
         const uint32_t T = s_ticket;
@@ -804,9 +822,15 @@ constexpr int kGroups = kS * kWaves;
 constexpr int kStageWave = BLT_STAGE_WAVE;    // the LDS the table leaves, shared by the waves
 // Look-back windows of 64 status words per round trip.  (Measured: 2 or 4 windows cost more
 // through register spills than the extra round trips they save.)
-constexpr int kLbWin = 1;
+#ifndef BLT_LBWIN
+#define BLT_LBWIN 1
+#endif
+constexpr int kLbWin = BLT_LBWIN;
+// Look-backs publish the inclusive prefixes of the tiles they fold (win_upgrade).
+#ifndef BLT_LB_UPGRADE
+#define BLT_LB_UPGRADE 1
+#endif
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint32_t kLbSpinLimit = 1u << 18;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
 static_assert(kGroups <= 64, "one lane per group in the tile resolve");
@@ -1139,9 +1163,12 @@ __device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lan
 }
 
 // Function of the aggregates in lanes [0, lim) of one window (lane 0 newest) applied to
-// carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.
+// carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.  With `lane_cin`
+// / `lane_scan` it also gives each lane its tile's carry-in and the inclusive (lane 0 up) scan of
+// the lanes' counts (for win_upgrade).
 __device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot,
-                                              uint32_t& live) {
+                                              uint32_t& live, uint32_t* lane_cin = nullptr,
+                                              uint32_t* lane_scan = nullptr) {
     const bool in = lane < lim;
     live |= __ballot(in && (s & kStLiveAgg) != 0) != 0;
     const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
@@ -1163,8 +1190,34 @@ __device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uin
         cin = older ? (uint32_t)((comask >> __builtin_ctzll(older)) & 1ull) : c;
     }
     const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x1FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
-    tot += lane_u32(wave_scan(cnt), 63);
+    const uint32_t scan = wave_scan(cnt);
+    tot += lane_u32(scan, 63);
+    if (lane_cin) { *lane_cin = cin; *lane_scan = scan; }
     return nonid ? (uint32_t)((comask >> __builtin_ctzll(nonid)) & 1ull) : c;
+}
+
+// Inclusive-prefix upgrade (round 4).  A look-back that found the inclusive prefix of lane lim's
+// tile (offset obase, live bit lbase) and folded the aggregates of lanes [0, lim) knows the
+// inclusive prefix of every one of those tiles too, and publishes it for each lane whose word is
+// still an aggregate: one masked 8-byte store per lane, the same value the tile's owner publishes
+// after its own look-back (the prefix is a function of the input alone), so racing writers agree and
+// a word only ever moves from aggregate to inclusive.  Without it the nearest inclusive prefix lies
+// where the previous generation of tiles left one (every tile of the current one looks back at
+// about the same time): 18 tiles back on average on cfg3, and 45 % of look-backs found none in 64
+// and paid another status round trip.  kBase: tile index of lane 0.
+__device__ __forceinline__ void win_upgrade(const PassParams& p, uint64_t s, int lim, int lane, int64_t kbase,
+                                            uint64_t obase, uint32_t lbase, uint32_t cin, uint32_t scan) {
+    const bool in = lane < lim;
+    const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
+    const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x1FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
+    const uint32_t total = lane_u32(scan, 63);
+    const uint32_t suffix = total - scan + cnt;   // tokens of lanes [lane, lim): this tile and the older ones
+    const bool ident = ((hi >> 28) & 3u) == 2u;
+    const uint32_t cout = ident ? cin : (hi >> 28) & 1u;   // a non-identity function is constant
+    const uint64_t lmask = __ballot(in && (s & kStLiveAgg) != 0);
+    const bool live = lbase || (lmask >> lane) != 0;
+    if (in && (s >> 62) == 1u)
+        st_publish(p.status + (kbase - lane), st_incl(cout, obase + suffix) | (live ? kStLiveIncl : 0ull));
 }
 
 struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never indexed (no alloca)
@@ -1178,6 +1231,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
     TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
     int64_t k = (int64_t)Tp - 1;
     uint32_t rounds = 0;
+    SpinClock clk;
     for (;;) {
         int qs = -1, f = 64;
         bool ready = true;
@@ -1206,7 +1260,8 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
             *bad_out = d;
         }
         if (!ready) {
-            if (++spins > kLbSpinLimit) {   // flagged; the tile writes nothing (C = 2)
+            ++spins;
+            if (clk.expired()) {   // flagged; the tile writes nothing (C = 2)
                 if (lane == 0) flag_error(p.ctl, KARG(sticky), 1u);
                 C = 2u; O = 0ull;
                 return;
@@ -1242,8 +1297,16 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 const uint64_t sf = ((uint64_t)lane_u32((uint32_t)(s[q] >> 32), f) << 32) | lane_u32((uint32_t)s[q], f);
                 c = (uint32_t)(sf >> 61) & 1u;
                 off = sf & (kStLiveIncl - 1ull);
-                live |= (sf & kStLiveIncl) != 0;
-                c = win_apply(s[q], f, lane, c, off, live);
+                const uint32_t lbase = (sf & kStLiveIncl) != 0;
+                live |= lbase;
+                if (BLT_LB_UPGRADE && f > 0) {
+                    const uint64_t obase = off;
+                    uint32_t cin, scan;
+                    c = win_apply(s[q], f, lane, c, off, live, &cin, &scan);
+                    win_upgrade(p, s[q], f, lane, k - 64 * q, obase, lbase, cin, scan);
+                } else {
+                    c = win_apply(s[q], f, lane, c, off, live);
+                }
             } else {
                 c = win_apply(s[q], 64, lane, c, off, live);
             }
@@ -1565,7 +1628,6 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 // condition; rings of kRing slots cover the at most two iterations of drift the chain allows
 // (a wave emits iteration i only after tile i-1 is resolved, which needs every wave's phase 1).
 constexpr int kRing = 4;
-constexpr uint32_t kWaitLimit = 1u << 22;
 // Per-wave phase stamps and look-back timing (tools/tile_timing.py) only in the timing build
 // (-DBLT_TIMING): kept live across the loop they cost scalar registers the kernel has none of.
 #ifdef BLT_TIMING
@@ -1588,9 +1650,9 @@ __device__ __forceinline__ void lds_release(uint32_t* f, uint32_t v) {
 }
 // Waits until *f >= v; on a (never expected) timeout flags error bit 8 and lets the wave go on.
 __device__ __forceinline__ void wait_ge(const PassParams& p, const uint32_t* f, uint32_t v) {
-    uint32_t spins = 0;
+    SpinClock clk;
     while (lds_acquire(f) < v) {
-        if (++spins > kWaitLimit) {
+        if (clk.expired()) {
             if ((threadIdx.x & 63) == 0) flag_error(p.ctl, KARG(sticky), 8u);
             break;
         }
@@ -1637,7 +1699,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
     const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
-    if (ws_refused(p, ntiles)) return;
+    const uint32_t cover = ws_cover(p);
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
     if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
@@ -1672,6 +1734,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     uint32_t T = uni(s_tk[kRing - 2]);    // tile in phase 1
     uint32_t Tp = kNone;                  // tile waiting for emission
     uint32_t Tq = uni(s_tk[kRing - 1]);   // the tile after T (its bytes load during T's iteration)
+    if (ws_refused(p, ntiles, cover)) T = kNone;   // (its two tickets are dropped: the reset zeroes them)
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     TInfo ti = {}, tip = {};
     if (T < ntiles) ti = tile_info(p, T);

@@ -928,3 +928,40 @@ def test_general_map_async_enqueue(name):
         assert 2 * tok == exp.size, (name, sync)
         assert np.array_equal(d_out[:2 * tok].cpu().numpy(), exp), (name, sync)
         assert np.array_equal(np.diff(offs) * 2, elens), (name, sync)
+
+
+def test_concurrent_scans_behind_busy_kernel():
+    """two handles' byte scans enqueued at once on two streams of one device, behind
+    ~0.1 s of matrix products on a third stream that occupy the CUs first.  The look-back and wave
+    waits time out on wall-clock time (200 ms, s_memrealtime), not on a count of sleeps, so a scan
+    whose workgroups share the device with other work finishes without a flag: both outputs
+    bit-exact, both workspaces and both handles' sticky words clean."""
+    import torch
+    rng = np.random.default_rng(77)
+    n = 48 << 20
+    texts = [synth.text(n, seed=11), rng.integers(0, 256, n, dtype=np.uint8)]
+    maps = [synth.merges_dict(synth.top_pair_merges(texts[0][:1 << 22], 300)),
+            {(int(a), int(b)): 256 + i for i, (a, b) in enumerate(rng.integers(0, 256, (30000, 2)))}]
+    cs = 16 << 20
+    strategies = [blt_amd.BpeStrategy(m) for m in maps]
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    bufs = []
+    for s, t in zip(strategies, texts):
+        wsb = s.workspace_size(n, cs)
+        bufs.append((torch.from_numpy(t).cuda(), torch.zeros(2 * n, dtype=torch.uint8, device="cuda"),
+                     torch.zeros(wsb, dtype=torch.uint8, device="cuda"), wsb))
+    a = torch.randn(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(streams[2]):
+        x = a
+        for _ in range(40):
+            x = torch.tanh(x @ a)
+    for s, st, (d_in, d_out, ws, wsb) in zip(strategies, streams, bufs):
+        s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, st.cuda_stream, sync=False)
+    torch.cuda.synchronize()
+    for s, st, m, t, (d_in, d_out, ws, wsb) in zip(strategies, streams, maps, texts, bufs):
+        s.check_workspace(ws.data_ptr(), st.cuda_stream)
+        assert not s.clear_error()
+        exp = O.COracle(m).run(t, cs, threads=16)
+        assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    assert torch.isfinite(x).all().item()
