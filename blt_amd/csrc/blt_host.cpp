@@ -577,8 +577,11 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
-    uint64_t ctl, status, total, off_a, off_b, cmap, bytes, zero_bytes;
+    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, bytes, zero_bytes;
 };
+// Chain block of a general map (right after pass 1's status words): u64 pass totals [2], u32 done
+// word, u32 fused-fail word, u64 final total, u32 finish-gate word, pad.
+constexpr uint64_t kChainBlock = 48;
 
 // Workspace: control block and look-back status words (zeroed before each pass), then for a
 // general map the pass totals and done flag, two chunk-offset arrays (the passes alternate) and
@@ -593,12 +596,13 @@ WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     L.ctl = 0;
     L.status = blt::kCtlBytes;
     L.zero_bytes = up16(blt::kCtlBytes + 8 * L.ntiles);
-    L.total = L.zero_bytes;   // u64 [2] pass totals (alternating), u32 done flag, pad: 32 bytes
-                              // (right after pass 1's status words: encode_device zeroes both at once)
-    L.off_a = L.total + 32;
+    L.total = L.zero_bytes;   // the chain block (kChainBlock bytes, right after pass 1's status
+                              // words: encode_device zeroes both at once)
+    L.off_a = L.total + kChainBlock;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
-    L.bytes = single_pass ? L.cmap : L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
+    L.gstat = L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));   // finish: a status word per group
+    L.bytes = single_pass ? L.cmap : L.gstat + up16(8 * L.nchunks);
     return L;
 }
 
@@ -726,6 +730,39 @@ int run_fused(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint
     return 0;
 }
 
+// The rest of a general map's chain from u16 pass k on, per group of chunks in LDS (blt::launch_finish):
+// tokens in place in d_out, chunk starts from the previous pass's offsets, this pass's offsets and
+// total as pass k's.  Enqueued once per encode, at the first pass whose input chunks may fit in LDS
+// (a pass at least halves a chunk's tokens: they hold >= cs >> k entering u16 pass k); when a group
+// does not fit after all, the gate leaves it to the ordinary pass k enqueued right behind it.
+int run_finish(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
+               uint8_t* d_out, uint32_t k, const uint64_t* off_in, uint64_t* off_out, uint64_t* total, uint32_t* done) {
+    blt::PassParams p{};
+    p.in = d_out;
+    p.out = d_out;
+    p.cstart = off_in;
+    p.nchunks = L.nchunks;
+    p.chunk_off = off_out;
+    p.total = total;
+    p.done = done;
+    p.pass_id = k;
+    p.status = reinterpret_cast<uint64_t*>(ws + L.gstat);
+    p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
+    p.hbuckets = t->hbuckets;
+    p.hmul1 = h->hmul1;
+    p.hmul2 = h->hmul2;
+    p.hshift = h->hshift;
+    p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
+    p.hone = h->hone ? 1u : 0u;
+    p.sticky = h->sticky.load(std::memory_order_acquire);
+    p.fin_gate = reinterpret_cast<uint32_t*>(ws + L.total + 32);
+    HIP_TRY(blt::launch_finish(p, dev, s));
+    return 0;
+}
+
+// Test hook (blt_debug_set_finish): 0 disables the finish kernels (the chain's ordinary passes only).
+std::atomic<int> g_finish{1};
+
 // A device error flagged during a general map's chain: the sticky message, with the control
 // block's flags and first-error record when they survive.  The u16 scan passes keep them (their
 // chunk-map kernel resets only the ticket); a generic u16 pass (merge_tokens_kernel, chunks under
@@ -793,7 +830,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     uint32_t* done = reinterpret_cast<uint32_t*>(ws + L.total + 16);
     // pass 1's control block and status words and the chain's totals are contiguous: one memset
     // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
-    HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + 32, s));
+    HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + kChainBlock, s));
     const bool bounded = h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1;
     // Passes 1 and 2 in one kernel (run_fused) when the bucket table fits in LDS, chunks hold whole
     // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
@@ -837,6 +874,13 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     };
     t_last_fused = fused ? 1 : 0;
     uint64_t rec[4] = {0, 0, 0, 0};
+    // the finish kernels, once per encode: at the first u16 pass whose input chunks may fit in LDS
+    bool fin_tried = !g_finish.load(std::memory_order_relaxed);
+    auto finish_now = [&](uint64_t kk) {
+        if (fin_tried || kk >= 64 || (cs >> kk) > blt::kFinCapTokens) return false;
+        fin_tried = true;
+        return true;
+    };
     if (bounded) {
         // a bounded chain (no value can be made from itself): u16 passes 1 .. depth - 1 are all a
         // pass can need, enqueued without reading the device's pass count; passes after the one
@@ -845,6 +889,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         const uint32_t k_last = h->chain_depth - 1;
         for (; k <= k_last; ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
+            if (finish_now(k))
+                if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
+                    return rc;
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
                                   false, &c, scan))
@@ -866,6 +913,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
+            if (finish_now(k))
+                if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
+                    return rc;
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
                                   false, &c, scan))
@@ -1467,6 +1517,10 @@ int blt_debug_byte_mode(const blt_bpe* h) {
     if (!h) return -1;
     return (h->byte_mode & 0xFF) | (h->allmerge ? 0x100 : 0) | (h->live_first ? 0x200 : 0);
 }
+
+// Not in the public header (tests): 0 disables the finish kernels of a general map's chain, 1 (the
+// default) enables them; returns the previous setting.
+int blt_debug_set_finish(int on) { return g_finish.exchange(on ? 1 : 0); }
 
 // Not in the public header: a general map's longest merge chain (0: single-pass, or unbounded).
 uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0; }

@@ -64,6 +64,7 @@ struct PassParams {
                                // marks a merge valued its own first byte
     uint32_t* sticky;          // the handle's pinned host error word (nullable): set to 1 with the
                                // error bits in ctl[1], so the handle's next call fails
+    uint32_t* fin_gate;        // finish kernels: the longest chunk's tokens (capped), from the gate kernel
     uint32_t ws_check;         // single-pass byte kernels launched without a memset (BLT_ENCODE_WORKSPACE_ZEROED):
                                // refuse (error bit 32, no output) when ntiles > ctl[kCtlCover]
     uint32_t* fused_fail;      // fused passes 1 + 2: set to 1 when a wave range's halo holds no
@@ -96,6 +97,14 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
 // offset go through the u16 scan's look-back.  Writes p.total, p.chunk_off and p.done as u16 pass
 // p.pass_id (1), or sets *p.fused_fail.
 hipError_t launch_scan_fused(const PassParams& p, int device, hipStream_t s);
+// The rest of a general map's chain from u16 pass p.pass_id on, per group of chunks in LDS
+// (finish_gate_kernel, finish_chunks_kernel): in place in p.out (= p.in), chunk starts from p.cstart
+// (the previous pass's offsets), status words at p.status (one per chunk), ticket p.ctl[0]; writes
+// p.chunk_off, p.total and p.done = p.pass_id, or nothing when the longest chunk does not fit in LDS
+// (the gate word *p.fin_gate, the longest chunk, must be zero before the launch).
+hipError_t launch_finish(const PassParams& p, int device, hipStream_t s);
+constexpr uint64_t kFinCapTokens = 16384;      // tokens of a group in LDS (finish_chunks_kernel)
+constexpr uint32_t kFinMaxGroupChunks = 1024;  // chunks per group
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s);
 // The end of a general map's chain enqueued up to its known depth: the final pass (the done word's,
 // else k_last) gives *tot_final and, when it wrote off1, the caller's chunk offsets.

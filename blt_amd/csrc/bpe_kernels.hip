@@ -2696,6 +2696,209 @@ __global__ __launch_bounds__(256) void chain_final_kernel(const uint64_t* tot, c
     if (chunk_off && (k & 1u) && i <= nchunks) chunk_off[i] = off1[i];
 }
 
+// ===========================================================================================
+// The rest of a general map's chain in one launch (round 4).  Once a pass leaves chunks small,
+// a u16 pass is mostly fixed cost (launch, chunk map, tickets, a look-back round trip; 11-18 us on
+// a few thousand tokens), and a 24-level chain paid it 14 times.  finish_chunks_kernel takes a
+// group of consecutive chunks per workgroup, holds their tokens in LDS and runs greedy passes over
+// them until one merges nothing (tokenizer.rs:63-86 per chunk: a pass that merges nothing in a
+// chunk leaves it as it is, so running the group to its fixpoint runs every chunk to its own), then
+// places the group's final tokens by a decoupled look-back over the groups' token counts.  Chunk
+// ends cut pairs as in the other passes (a chunk's first token always lands).
+//
+// In place: a group writes its final tokens only after its look-back, i.e. after every earlier
+// group published its count, which each does after reading its input into LDS; and it writes below
+// the next group's input (final prefixes never exceed the input's).  Groups come from a ticket, so
+// the lowest unfinished group always has a running workgroup.
+//
+// finish_gate_kernel runs first: it checks every group fits in LDS (else the finish kernel returns
+// at once and the ordinary passes the host enqueued behind it run), zeroes the groups' status
+// words and the ticket.  Both return at once when an earlier pass was final.
+// ===========================================================================================
+constexpr uint32_t kFinThreads = 1024;
+constexpr uint32_t kFinCap = kFinThreads * 16;   // tokens of a group in LDS (one 16-token segment per lane)
+constexpr uint32_t kFinMaxChunks = 1024;         // chunks per group
+
+// Chunks per group from the longest chunk (the gate's word): as many as surely fit in LDS together.
+__device__ __forceinline__ uint32_t fin_group_of(uint32_t lmax) {
+    const uint32_t g = kFinCap / (lmax ? lmax : 1u);
+    return g < 1u ? 1u : (g > kFinMaxChunks ? kFinMaxChunks : g);
+}
+
+// One thread per chunk: the longest chunk into the gate word (capped at kFinCap + 1: too long),
+// the chunk's group status word zeroed (groups never outnumber chunks), the ticket zeroed.
+__global__ __launch_bounds__(256) void finish_gate_kernel(PassParams p) {
+    if (seg::pass_done(p)) return;
+    const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (c == 0) p.ctl[0] = 0u;
+    if (c >= p.nchunks) return;
+    p.status[c] = 0ull;
+    const uint64_t len = p.cstart[c + 1] - p.cstart[c];
+    atomicMax(p.fin_gate, (uint32_t)(len > kFinCap ? kFinCap + 1u : len));
+}
+
+template <int kHash>
+__global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint2 s_fhash[];
+    __shared__ __attribute__((aligned(16))) uint16_t s_tok[2][kFinCap + 16];
+    __shared__ uint32_t s_cpos[2][kFinMaxChunks + 1];   // chunk starts in the group's tokens, [nc] = count
+    __shared__ uint32_t s_wfn[kFinThreads / 64][4];
+    __shared__ uint32_t s_gin[kFinThreads / 64][2];    // per wave: carry-in, tokens before it
+    __shared__ uint32_t s_cnt;
+    __shared__ uint32_t s_g;
+    __shared__ uint64_t s_O;
+    if (seg::pass_done(p)) return;
+    const uint32_t lmax = __hip_atomic_load(p.fin_gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lmax > kFinCap) return;   // a chunk too long for LDS: the ordinary passes run
+    const uint32_t grp = fin_group_of(lmax);
+    const uint64_t ngroups = (p.nchunks + grp - 1) / grp;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int kW = kFinThreads / 64;
+    if constexpr (kHash != 0) {
+        const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
+        uint4* dst = reinterpret_cast<uint4*>(s_fhash);
+        for (uint32_t i = tid; i < p.hbytes / 16u; i += kFinThreads) dst[i] = src[i];
+    }
+    // persistent: groups from the ticket, in order, until none is left
+    for (;;) {
+    __syncthreads();
+    if (tid == 0) s_g = atomicAdd(p.ctl, 1u);
+    __syncthreads();
+    const uint64_t g = s_g;
+    if (g >= ngroups) return;
+    const uint64_t c0 = g * grp, c1 = c0 + grp < p.nchunks ? c0 + grp : p.nchunks;
+    const uint32_t nc = (uint32_t)(c1 - c0);
+    const uint64_t S = p.cstart[c0];
+    uint32_t n = (uint32_t)(p.cstart[c1] - S);   // <= kFinCap (the gate)
+    const uint16_t* in = reinterpret_cast<const uint16_t*>(p.in);
+    for (uint32_t i = tid; i <= nc; i += kFinThreads) s_cpos[0][i] = (uint32_t)(p.cstart[c0 + i] - S);
+    for (uint32_t i = tid; i < kFinCap + 16; i += kFinThreads) s_tok[0][i] = i < n ? in[S + i] : (uint16_t)0;
+    const uint32_t tab = kHash != 0 ? seg::lds_addr(s_fhash) : 0u;
+    __syncthreads();
+
+    uint32_t cur = 0;
+    const uint32_t pos0 = 16u * (uint32_t)tid;
+    for (;;) {
+        // one greedy pass over s_tok[cur][0, n) into s_tok[cur ^ 1]
+        uint32_t x[8];
+        {
+            const uint4 a = *reinterpret_cast<const uint4*>(&s_tok[cur][pos0]);
+            const uint4 b = *reinterpret_cast<const uint4*>(&s_tok[cur][pos0 + 8]);
+            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+        }
+        const uint32_t nxt = s_tok[cur][pos0 + 16];
+        // pairs (i, i + 1) that may merge: i + 1 < n and i + 1 not a chunk start
+        const int32_t rr = (int32_t)n - (int32_t)pos0;
+        const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
+        uint32_t pairs = (vmask >> 1) | (rr > 16 ? 0x8000u : 0u);
+        uint32_t a_lo = 0;   // first chunk start >= pos0 + 1 (index into s_cpos)
+        if (nc > 1) {
+            uint32_t lo = 0, hi = nc;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_cpos[cur][mid] < pos0 + 1u) lo = mid + 1; else hi = mid;
+            }
+            a_lo = lo;
+            for (uint32_t a = lo; a < nc; ++a) {
+                const uint32_t b = s_cpos[cur][a];
+                if (b > pos0 + 16u) break;
+                pairs &= ~(1u << (b - 1u - pos0));
+            }
+        }
+        uint32_t v[8], m = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int h = k >> 1;
+            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
+            const uint32_t r = seg::tok_get<kHash>(p, tab, key);
+            const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
+            m |= (uint32_t)hit << k;
+            const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
+            if (k & 1) v[h] |= t << 16; else v[h] = t;
+        }
+        const uint32_t ident = m == 0xFFFFu;
+        const uint32_t M1 = merges_for(m, 1u), M0 = merges_for(m, 0u);
+        const uint32_t cnt1 = __popc(lands_for(M1, 1u, vmask));
+        const uint32_t cnt0 = __popc(lands_for(M0, 0u, vmask));
+        const uint32_t cout = ((M1 >> 15) & 1u) ^ 1u;
+        uint32_t hasb, bco, excl;
+        WaveFn fn;
+        resolve_wave(ident, cout, cnt0, cnt1, lane, hasb, bco, excl, fn);
+        if (lane == 0) { s_wfn[wave][0] = fn.ident; s_wfn[wave][1] = fn.cout; s_wfn[wave][2] = fn.cnt0; s_wfn[wave][3] = fn.cnt1; }
+        __syncthreads();
+        if (wave == 0) {
+            uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
+            if (lane < kW) { gi = s_wfn[lane][0]; gco = s_wfn[lane][1]; g0 = s_wfn[lane][2]; g1 = s_wfn[lane][3]; }
+            uint32_t ghb, gbc, gex;
+            WaveFn tf;
+            resolve_wave(gi, gco, g0, g1, lane, ghb, gbc, gex, tf);
+            // the group's first token lands (carry-in 1): the high halves
+            if (lane < kW) { s_gin[lane][0] = ghb ? gbc : 1u; s_gin[lane][1] = gex >> 16; }
+            if (lane == 0) s_cnt = tf.cnt1;
+        }
+        __syncthreads();
+        const uint32_t cg = s_gin[wave][0];
+        const uint32_t c = hasb ? bco : cg;
+        const uint32_t lane_off = s_gin[wave][1] + (cg ? (excl >> 16) : (excl & 0xFFFFu));
+        const uint32_t M = merges_for(m, c);
+        const uint32_t L = lands_for(M, c, vmask);
+        const uint32_t ncnt = s_cnt;
+        if (ncnt != n) {   // uniform: something merged
+            if (vmask) seg::stage_b16(v, L, seg::lds_addr(&s_tok[cur ^ 1][0]) + 2u * lane_off);
+            // chunk starts in [pos0, pos0 + 16) land: their new positions
+            if (nc > 1) {
+                for (uint32_t a = a_lo > 0 ? a_lo - 1 : 0; a < nc; ++a) {
+                    const uint32_t b = s_cpos[cur][a];
+                    if (b >= pos0 + 16u) break;
+                    if (b >= pos0) s_cpos[cur ^ 1][a] = lane_off + __popc(L & ((1u << (b - pos0)) - 1u));
+                }
+            }
+            if (tid == 0) { s_cpos[cur ^ 1][0] = 0u; s_cpos[cur ^ 1][nc] = ncnt; }
+        }
+        __syncthreads();
+        if (ncnt == n) break;   // this pass merged nothing: every chunk of the group is at its fixpoint
+        // tokens past the new count must not look like a pair for the next pass's last lanes (masked)
+        cur ^= 1;
+        n = ncnt;
+    }
+
+    // place the group: its count as an aggregate (constant carry 1: chunks never merge across), the
+    // look-back over the groups before it, then its tokens, chunk offsets and (last group) the total
+    if (wave == 0) {
+        uint32_t C = 1u, how = 0, spins = 0, live = 0;
+        uint64_t O = 0;
+        if (g == 0) {
+            if (lane == 0) st_publish(p.status, st_incl(1u, n));
+        } else {
+            if (lane == 0) st_publish(p.status + g, st_agg(1u, 1u, n, n));
+            uint64_t lbs[seg::kLbWin];
+            seg::lb_issue(p, (int64_t)g - 1, lane, lbs);
+            seg::lb_finish(p, (uint32_t)g, lane, lbs, C, O, how, spins, live);
+            if (lane == 0) {
+                if (C > 1u || O > S) {   // a failed look-back (flagged) or a broken prefix: write nothing
+                    if (C <= 1u) record_error(p, 4u, (uint32_t)g, 0xFEu, O, n, C);
+                    O = ~0ull;
+                } else {
+                    st_publish(p.status + g, st_incl(1u, O + n));
+                }
+            }
+        }
+        if (lane == 0) s_O = O;
+    }
+    __syncthreads();
+    const uint64_t O = s_O;
+    if (O == ~0ull) continue;
+    uint16_t* out = reinterpret_cast<uint16_t*>(p.out);
+    for (uint32_t i = tid; i < n; i += kFinThreads) out[O + i] = s_tok[cur][i];
+    for (uint32_t i = tid; i < nc; i += kFinThreads) p.chunk_off[c0 + i] = O + s_cpos[cur][i];
+    if (c1 == p.nchunks && tid == 0) {
+        p.chunk_off[p.nchunks] = O + n;
+        *p.total = O + n;
+        *p.done = p.pass_id;
+    }
+    }   // groups
+}
+
 __global__ void inject_error_kernel(uint32_t* ctl, uint32_t* sticky) {
     if (threadIdx.x == 0) flag_error(ctl, sticky, 1u);
 }
@@ -2837,6 +3040,23 @@ hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const u
     const uint64_t blocks = chunk_off ? (nchunks + 1 + 255) / 256 : 1;
     hipLaunchKernelGGL(chain_final_kernel, dim3((unsigned)blocks), dim3(256), 0, s, tot, done, off1, chunk_off, nchunks,
                        k_last, tot_final);
+    return hipGetLastError();
+}
+
+hipError_t launch_finish(const PassParams& p, int device, hipStream_t s) {
+    if (p.nchunks == 0 || !p.fin_gate || p.nchunks > 0xFFFFFFFFull * 256u) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(finish_gate_kernel, dim3((unsigned)((p.nchunks + 255) / 256)), dim3(256), 0, s, p);
+    const bool lds = p.hbytes <= kHashLdsMax;
+    const int mode = lds ? (p.hone ? 2 : 1) : 0;
+    const size_t smem = lds ? (size_t)p.hbytes : 0;
+    // persistent: one workgroup per CU (its LDS), no more than there are chunks
+    const void* fn = mode == 2 ? (const void*)finish_chunks_kernel<2>
+                     : mode == 1 ? (const void*)finish_chunks_kernel<1> : (const void*)finish_chunks_kernel<0>;
+    const int grid = grid_for_smem((uint32_t)std::min<uint64_t>(p.nchunks, 0xFFFFFFFFull), device, fn, kFinThreads, smem);
+    const dim3 g((unsigned)grid), b(kFinThreads);
+    if (mode == 2) hipLaunchKernelGGL((finish_chunks_kernel<2>), g, b, smem, s, p);
+    else if (mode == 1) hipLaunchKernelGGL((finish_chunks_kernel<1>), g, b, smem, s, p);
+    else hipLaunchKernelGGL((finish_chunks_kernel<0>), g, b, 0, s, p);
     return hipGetLastError();
 }
 

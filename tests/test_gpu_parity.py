@@ -965,3 +965,80 @@ def test_concurrent_scans_behind_busy_kernel():
         exp = O.COracle(m).run(t, cs, threads=16)
         assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
     assert torch.isfinite(x).all().item()
+
+
+def _finish(on):
+    return blt_amd._lib.lib().blt_debug_set_finish(1 if on else 0)
+
+
+@pytest.mark.parametrize("case", ["chain_cs16k", "chain_groups", "text_small_chunks", "gate_fails", "wide_map",
+                                  "cyclic_small", "two_choice_lds"])
+def test_finish_kernel_fixpoint(case):
+    """Round 4: the rest of a general map's chain in one launch once chunks may fit in LDS
+    (finish_chunks_kernel: a group of chunks per workgroup, greedy passes in LDS to the fixpoint,
+    then a look-back over the groups' counts).  Against the oracle and against the chain run with
+    the finish kernels disabled: chunk sizes where one chunk fills LDS exactly, many chunks per
+    group (chunk starts inside a group, ragged last group), a gate that fails (chunks that did not
+    shrink: the ordinary passes run), a map too large for LDS (the table read from L2), a cyclic map
+    (host-checked batches) and the 2-choice LDS table, with the chunk offsets of the device API."""
+    import torch
+    rng = np.random.default_rng(abs(hash(case)) % (1 << 31))
+    if case == "chain_cs16k":      # 'a' runs, 32 KiB chunks: after the byte pass 16384 tokens per chunk
+        m, cs = synth.doubling_chain(10), 32768
+        data = np.full(20 * cs + 999, 97, np.uint8)
+    elif case == "chain_groups":   # 1000-byte chunks: up to 32 chunks per group, a ragged last group
+        m, cs = synth.doubling_chain(8), 1000
+        data = np.full(300_017, 97, np.uint8)
+        data[rng.choice(data.size, 3000, replace=False)] = 98
+    elif case == "text_small_chunks":
+        m, cs = CHAINED_TEXT_MAP, 4099
+        data = synth.text((1 << 20) + 77, seed=91)
+    elif case == "gate_fails":     # chunks barely shrink: eligible by size bound, too large in fact
+        m, cs = {(97, 98): 97, (99, 100): 256, (256, 101): 99}, 40000
+        data = rng.choice(np.array([97, 98, 99, 100, 101, 102], np.uint8), 400_003)
+    elif case == "wide_map":       # > 48 KiB of buckets: the finish kernel reads the table from L2
+        m = {(int(a), int(b)): 256 + i for i, (a, b) in enumerate(rng.integers(97, 105, (60, 2)))}
+        m.update({(256 + i, 256 + j): 400 + 64 * i + j for i in range(60) for j in range(60)})
+        m.update({(int(a), int(b)): 5000 + i for i, (a, b) in enumerate(rng.integers(0, 256, (6000, 2)))
+                  if (int(a), int(b)) not in m})
+        cs = 20000
+        data = rng.integers(97, 105, 500_001, dtype=np.uint8)
+    elif case == "cyclic_small":   # (97, 98) -> 97 needs one pass per 'b' of a run: host-checked batches
+        m, cs = {(97, 98): 97, (98, 98): 256}, 5000
+        data = rng.choice(np.array([97, 98, 98, 98, 99], np.uint8), 200_000)
+    else:                          # 513..3071 keys: the 2-choice table in LDS
+        letters = range(97, 123)
+        m = {(a, b): 256 + i for i, (a, b) in enumerate((a, b) for a in letters for b in letters)}
+        for i in range(0, 676, 2):
+            m[(256 + i, 97 + i % 26)] = 2000 + i
+        cs = 8192
+        data = rng.integers(97, 123, 700_000, dtype=np.uint8)
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    n = data.size
+    nch = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    prev = _finish(True)
+    try:
+        for on in (True, False):
+            _finish(on)
+            got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+            assert np.array_equal(got, exp), (case, on)
+            assert np.array_equal(lens, elens), (case, on)
+            for sync in (True, False):
+                d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+                d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+                wsb = s.workspace_size(n, cs)
+                ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+                s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream,
+                                d_off.data_ptr(), sync=sync)
+                torch.cuda.synchronize()
+                offs = d_off.cpu().numpy()
+                assert int(offs[-1]) * 2 == exp.size, (case, on, sync)
+                assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), (case, on, sync)
+                assert np.array_equal(np.diff(offs) * 2, elens), (case, on, sync)
+                s.check_workspace(ws.data_ptr(), stream)
+    finally:
+        _finish(prev)
