@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <chrono>
@@ -164,8 +165,34 @@ static double mono_now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Seconds from the process's start (exec) to now: /proc/self/stat's starttime (clock ticks since
+// boot) against CLOCK_BOOTTIME.  BLT_CLI_TIMING only: the exec, dynamic loading (the HIP runtime
+// libraries) and static constructors before main.
+static double since_exec() {
+    FILE* f = fopen("/proc/self/stat", "r");
+    if (!f) return -1.0;
+    char buf[2048];
+    const size_t len = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[len] = 0;
+    const char* q = strrchr(buf, ')');   // comm may hold spaces
+    if (!q) return -1.0;
+    unsigned long long start = 0;
+    int field = 2;
+    for (const char* c = q + 1; *c; ++c) {
+        if (*c == ' ') {
+            ++field;
+            if (field == 22) { start = strtoull(c + 1, nullptr, 10); break; }
+        }
+    }
+    timespec bt;
+    clock_gettime(CLOCK_BOOTTIME, &bt);
+    return (double)bt.tv_sec + 1e-9 * (double)bt.tv_nsec - (double)start / (double)sysconf(_SC_CLK_TCK);
+}
+
 int main(int argc, char** argv) {
     const double t_main = mono_now();
+    const double t_exec = getenv("BLT_CLI_TIMING") ? since_exec() : 0.0;
     const Args a = parse_args(argc, argv);
 
     // CoreConfig::new_from_cli (lib.rs:149-174): threads, chunk size string, merges file
@@ -193,6 +220,8 @@ int main(int argc, char** argv) {
     cfg.chunk_size = cs;
     cfg.n_gpus = a.gpus;
     const double t_run = mono_now();
+    if (getenv("BLT_CLI_TIMING"))
+        fprintf(stderr, "blt timing: exec -> main %.4f s, merges loaded at %.4f s\n", t_exec, t_run - t_main);
     const int rc = blt_run_tokenizer(&cfg);
     const double t_done = mono_now();
     if (rc) run_error(lib_error(rc));

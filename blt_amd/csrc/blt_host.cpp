@@ -756,6 +756,7 @@ int run_finish(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     p.hone = h->hone ? 1u : 0u;
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.fin_gate = reinterpret_cast<uint32_t*>(ws + L.total + 32);
+    p.debug = g_debug_tiles;
     HIP_TRY(blt::launch_finish(p, dev, s));
     return 0;
 }

@@ -227,6 +227,64 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
     return 0;
 }
 
+// Direct path for a regular output file this run created (round 4): the file is sized to the
+// output's bound (ftruncate), mapped shared, and the whole input is tokenised in ONE library call
+// straight into the mapping at its final offset (blt_bpe_process_chunks pipelines its windows over
+// the devices and writes each window's tokens in chunk order, pipeline.rs:153-192), then the file
+// is cut to the bytes produced.  No host buffer and no write(2): the page-cache copy that bounded
+// the windowed path (one inode lock, ~5.5 GB/s on tmpfs) becomes the runtime's device-to-host
+// copies into pages the preallocation below already holds.  Returns 1 (nothing done) when the
+// file cannot be sized or mapped, so the caller takes the windowed path.
+int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, int fd, size_t head,
+                    const uint8_t* head_bytes) {
+    const size_t cap = st.kind == Strategy::kPassthrough ? n : 2 * n;
+    const size_t total = head + cap;
+    if (total == 0) return 0;
+    if (ftruncate(fd, (off_t)total) != 0) return 1;
+    void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) {
+        (void)ftruncate(fd, 0);
+        return 1;
+    }
+    uint8_t* out = static_cast<uint8_t*>(m);
+    if (head) memcpy(out, head_bytes, head);
+    size_t olen = 0;
+    int rc = 0;
+    if (n && st.kind == Strategy::kBpe) {
+        rc = blt_bpe_process_chunks(st.h, in, n, cs, st.gpus, out + head, cap, &olen, nullptr);
+    } else {
+        // passthrough and basic are position-wise (tokenizer.rs:108-124, :129-137): pieces of 256 MiB
+        constexpr size_t kPiece = size_t(256) << 20;
+        for (size_t off = 0; off < n && !rc; off += kPiece) {
+            const size_t len = std::min(kPiece, n - off);
+            size_t w = 0;
+            if (st.kind == Strategy::kPassthrough) {
+                memcpy(out + head + olen, in + off, len);
+                w = len;
+            } else {
+                rc = blt_basic_process_chunk(in + off, len, out + head + olen, cap - olen, &w);
+            }
+            olen += w;
+        }
+    }
+    munmap(m, total);
+    const std::string msg = rc ? last_error() : std::string();
+    // the bytes produced (an error leaves the content token only, like a run that wrote no chunk)
+    if (ftruncate(fd, (off_t)(head + (rc ? 0 : olen))) != 0 && !rc) return os_error(errno);
+    if (rc) return set_error(rc, "%s", msg.c_str());
+    return 0;
+}
+
+// Page allocation of the output file's first `bytes` ahead of the writes (FALLOC_FL_KEEP_SIZE: the
+// file's size is unchanged), on a helper thread while the HIP runtime starts: on tmpfs most of a
+// write's cost is allocating and zeroing pages (1 GiB: ~0.06 s to fallocate, then copies run ~2x
+// faster, profiles/r03_tmpfs_write.txt).  Best effort: an error leaves the writes to allocate.
+void preallocate(int fd, size_t bytes) {
+    constexpr size_t kStep = size_t(64) << 20;
+    for (size_t off = 0; off < bytes; off += kStep)
+        if (fallocate(fd, FALLOC_FL_KEEP_SIZE, (off_t)off, (off_t)std::min(kStep, bytes - off)) != 0) return;
+}
+
 // Stream path (pipeline.rs:196-433): one read per chunk, at most `threads` chunks in flight, a
 // worker pool tokenises (each call stages its chunk through the GPU; the handle is reentrant), a
 // writer emits results in chunk order.  Any error stops reading and is returned.
@@ -380,10 +438,21 @@ int run(const blt_run_config* c) {
         n = (size_t)sb.st_size;
         if (st.kind == Strategy::kBpe && n && !getenv("BLT_NO_PREWARM")) {   // (env: A/B runs)
             const size_t per = std::max<size_t>(1, (size_t(256) << 20) / cs);   // run_mmap's window
-            const uint64_t win = std::min<uint64_t>(n, (uint64_t)per * cs);
-            prewarm = std::thread([&st, &gpu_count, win, cs] {
+            // the mapped-output path tokenises the whole input in one call (run_mmap_direct)
+            const bool whole = c->output_path && !getenv("BLT_NO_DIRECT_OUTPUT");
+            const uint64_t win = whole ? (uint64_t)n : std::min<uint64_t>(n, (uint64_t)per * cs);
+            prewarm = std::thread([&st, &gpu_count, win, cs, timing, ts0] {
+                auto since = [&ts0] {
+                    timespec t;
+                    clock_gettime(CLOCK_MONOTONIC, &t);
+                    return (double)(t.tv_sec - ts0.tv_sec) + 1e-9 * (double)(t.tv_nsec - ts0.tv_nsec);
+                };
                 st.gpus = gpu_count(st.gpus);
+                const double t_rt = timing ? since() : 0;
                 blt_prewarm_chunks(st.h, win, cs, st.gpus);
+                if (timing)
+                    fprintf(stderr, "blt timing: prewarm: HIP runtime up at %.4f s, device tables and buffers at %.4f s\n",
+                            t_rt, since());
             });
         }
         if (n) {
@@ -410,17 +479,43 @@ int run(const blt_run_config* c) {
         size_t n;
         ~Unmap() { if (p) munmap(const_cast<uint8_t*>(p), n); }
     } unmap{map, n};
-    if (prewarm.joinable()) prewarm.join();
-    else if (st.kind == Strategy::kBpe) st.gpus = gpu_count(st.gpus);
 
-    // setup_output_writer (io_handler.rs:70-78): File::create truncates; None is stdout
+    // setup_output_writer (io_handler.rs:70-78): File::create truncates; None is stdout.  Created
+    // after the input (as the reference), but before the device is ready, so its pages can be
+    // allocated meanwhile.
     Sink sink;
     int ofd = 1;
     if (c->output_path) {
-        ofd = ::open(c->output_path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-        if (ofd < 0) return os_error(errno);
+        ofd = ::open(c->output_path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+        if (ofd < 0) {
+            const int e = errno;
+            if (prewarm.joinable()) prewarm.join();
+            return os_error(e);
+        }
         sink.fd = ofd;
         sink.positioned = true;
+    }
+    const size_t head = c->content_token ? 2 : 0;
+    // the mapped-output path: a file input (fixed chunks) into a regular output file this run created
+    bool direct = false;
+    if (c->input_path && c->output_path && !getenv("BLT_NO_DIRECT_OUTPUT")) {
+        struct stat ob;
+        direct = fstat(ofd, &ob) == 0 && S_ISREG(ob.st_mode);
+    }
+    std::thread prealloc;
+    if (direct && n) {
+        // expected output: basic 2 bytes per byte; BPE about 1 (large merge maps: ~0.5 tokens per byte)
+        const size_t est = head + (st.kind == Strategy::kBasic ? 2 * n : n);
+        prealloc = std::thread([ofd, est] { preallocate(ofd, est); });
+    }
+    if (prewarm.joinable()) prewarm.join();
+    else if (st.kind == Strategy::kBpe) st.gpus = gpu_count(st.gpus);
+    if (prealloc.joinable()) prealloc.join();
+    if (timing) {
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        fprintf(stderr, "blt timing: device ready and output preallocated at %.4f s\n",
+                (double)(t.tv_sec - ts0.tv_sec) + 1e-9 * (double)(t.tv_nsec - ts0.tv_nsec));
     }
     auto stamp = [&](const char* what) {
         if (!timing) return;
@@ -436,13 +531,17 @@ int run(const blt_run_config* c) {
     } closer{c->output_path ? ofd : -1};
 
     int rc = 0;
-    if (c->content_token) {   // prepend_content_type_token (lib.rs:284-293)
-        const uint8_t t[2] = {(uint8_t)(c->content_token >> 8), (uint8_t)c->content_token};
-        rc = sink.write_all(t, 2);
-    }
-    if (!rc) {
-        if (c->input_path) rc = run_mmap(st, map, n, cs, sink);
-        else rc = run_stream(st, 0, cs, (size_t)c->threads, sink);
+    const uint8_t tok[2] = {(uint8_t)(c->content_token >> 8), (uint8_t)c->content_token};
+    int drc = 1;
+    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok);
+    if (drc <= 0) {
+        rc = drc;
+    } else {
+        if (c->content_token) rc = sink.write_all(tok, 2);   // prepend_content_type_token (lib.rs:284-293)
+        if (!rc) {
+            if (c->input_path) rc = run_mmap(st, map, n, cs, sink);
+            else rc = run_stream(st, 0, cs, (size_t)c->threads, sink);
+        }
     }
     stamp("chunks written");
     if (!rc && c->output_path) {

@@ -1226,6 +1226,9 @@ struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never 
 };
 
 // live: OR of the live bits of every tile before Tp (u16 scan kernel; 0 in the byte pass).
+// Call it from wave-uniform control flow only (a branch on an SGPR value): its DPP scans
+// (row_bcast) need the whole wave, and measured in a kernel that reached it through a branch on a
+// VGPR value (finish_chunks_kernel's first version), the window sums came out wrong.
 __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (&s)[kLbWin], uint32_t& C,
                           uint64_t& O, uint32_t& how, uint32_t& spins, uint32_t& live, uint32_t* bad_out = nullptr) {
     TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
@@ -2737,6 +2740,50 @@ __global__ __launch_bounds__(256) void finish_gate_kernel(PassParams p) {
     atomicMax(p.fin_gate, (uint32_t)(len > kFinCap ? kFinCap + 1u : len));
 }
 
+// Look-back over the groups before g (one wave): windows of 64 status words, the counts of the
+// aggregates in front of the nearest inclusive prefix summed with a butterfly of lane shuffles.
+// Every group function is "carry 1, n tokens", so no carry chain is needed.
+__device__ __forceinline__ void fin_lookback(const PassParams& p, uint64_t g, int lane, uint32_t& C, uint64_t& O,
+                                             uint32_t& how, uint32_t& spins) {
+    int64_t k = (int64_t)g - 1;
+    uint64_t acc = 0;
+    uint32_t rounds = 0;
+    SpinClock clk;
+    for (;;) {
+        const int64_t idx = k - lane;
+        const uint64_t s = idx >= 0 ? st_read(p.status + idx) : st_incl(1u, 0ull);
+        const uint32_t flag = (uint32_t)(s >> 62);
+        const uint64_t inc = __ballot(flag == 2u), rdy = __ballot(flag != 0u);
+        const int f = inc ? (int)__builtin_ctzll(inc) : 64;
+        const uint64_t need = f >= 63 ? ~0ull : ((2ull << f) - 1ull);
+        if ((rdy & need) != need) {
+            ++spins;
+            if (clk.expired()) {
+                if (lane == 0) flag_error(p.ctl, KARG(sticky), 1u);
+                C = 2u;
+                O = 0ull;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t cnt = lane < f ? (uint32_t)(s & 0x3FFFFFFFull) : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d, 64);
+        acc += cnt;
+        if (f < 64) {
+            const uint64_t sf = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), f) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, f);
+            O = acc + (sf & (kStLiveIncl - 1ull));
+            C = 1u;
+            how = (uint32_t)f | (rounds << 8);
+            return;
+        }
+        k -= 64;
+        ++rounds;
+    }
+}
+
 template <int kHash>
 __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p) {
     extern __shared__ __attribute__((aligned(16))) uint2 s_fhash[];
@@ -2865,15 +2912,13 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     // place the group: its count as an aggregate (constant carry 1: chunks never merge across), the
     // look-back over the groups before it, then its tokens, chunk offsets and (last group) the total
     if (wave == 0) {
-        uint32_t C = 1u, how = 0, spins = 0, live = 0;
+        uint32_t C = 1u, how = 0, spins = 0;
         uint64_t O = 0;
         if (g == 0) {
             if (lane == 0) st_publish(p.status, st_incl(1u, n));
         } else {
             if (lane == 0) st_publish(p.status + g, st_agg(1u, 1u, n, n));
-            uint64_t lbs[seg::kLbWin];
-            seg::lb_issue(p, (int64_t)g - 1, lane, lbs);
-            seg::lb_finish(p, (uint32_t)g, lane, lbs, C, O, how, spins, live);
+            fin_lookback(p, g, lane, C, O, how, spins);
             if (lane == 0) {
                 if (C > 1u || O > S) {   // a failed look-back (flagged) or a broken prefix: write nothing
                     if (C <= 1u) record_error(p, 4u, (uint32_t)g, 0xFEu, O, n, C);
@@ -2883,7 +2928,18 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
                 }
             }
         }
-        if (lane == 0) s_O = O;
+        if (lane == 0) {
+            s_O = O;
+            if (p.debug) {   // tests only: the group's record
+                uint64_t* d = p.debug + 16ull * g;
+                d[0] = g; d[1] = S; d[2] = p.cstart[c1] - S; d[3] = n; d[4] = O;
+                d[5] = C | ((uint64_t)how << 8) | ((uint64_t)spins << 32);
+                d[6] = lmax | ((uint64_t)grp << 32); d[7] = nc;
+                d[8] = g ? st_read(p.status + g - 1) : 0; d[9] = st_read(p.status);
+                d[10] = st_read(p.status + g);
+                d[11] = g >= 2 ? st_read(p.status + g - 2) : 0;
+            }
+        }
     }
     __syncthreads();
     const uint64_t O = s_O;

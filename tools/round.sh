@@ -16,6 +16,8 @@
 #   proff2[:ROWS]      rocprofv3 kernel stats of the f2 rows (bench.py --only-configs ROWS)
 #   pmc:WL[:GROUPS]    tools/pmc_profile.py on bench.py --workload WL (groups default fetch,write,insts)
 #   pmcf2:ROW[:GROUPS] PMC of one f2 row (tools/f2_row.py: every kernel of its calls, traffic per call)
+#   cli[:ENV]          tools/cli_phases.py: the CLI's BLT_CLI_TIMING phases on 1 GiB, the HIP start-up probe
+#   py:SCRIPT[:ARGS]   a tool script under its own time limit
 #   resources          -Rpass-analysis=kernel-resource-usage of the kernel source (CPU only)
 set -e
 TAG=${1:?tag}
@@ -30,9 +32,10 @@ for st in "$@"; do
   echo "== $st $(date +%T)"
   case $kind in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 \
-        || { tail -40 "$O/tests.log"; exit 1; }
-      tail -2 "$O/tests.log" ;;
+      # tests[:K] runs only the tests whose names match K (pytest -k)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${a:+-k "$a"} \
+        > "$O/tests${a:+_$a}.log" 2>&1 || { tail -40 "$O/tests${a:+_$a}.log"; exit 1; }
+      tail -2 "$O/tests${a:+_$a}.log" ;;
     smoke)
       timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke()' > "$O/smoke.log" 2>&1
       tail -1 "$O/smoke.log" ;;
@@ -75,6 +78,17 @@ for st in "$@"; do
       timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --kernel "" --script tools/f2_row.py --calls 5 \
         --groups "${b:-fetch,write}" -- --row "$a" --reps 5 > "$O/pmc_$a.log" 2>&1
       grep -E "hbm_bytes_per_call|calls" "$O/pmc_$a/pmc_summary.json" ;;
+    cli)
+      # BLT_CLI_TIMING phases of the CLI on 1 GiB (tools/cli_phases.py), cli:ENV (NAME=VALUE, commas)
+      [ -x build/hip_init_probe ] || /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/hip_init_probe.cpp -o build/hip_init_probe
+      nb=$((nb + 1))
+      timeout -k 10 300 python tools/cli_phases.py --out "$O/cli_phases_$nb.json" ${a:+--env "$a"} > "$O/cli_$nb.log" 2>&1
+      python -c "import json;d=json.load(open('$O/cli_phases_$nb.json'));print(d.get('hip_init_probe'));[print(r['wall_s'],r['GBps']) for r in d['runs']]" ;;
+    py)
+      # any tool script: py:tools/x.py[:ARGS] (ARGS commas for spaces), output py_<n>.log
+      nb=$((nb + 1))
+      timeout -k 10 300 python -u "$a" ${b//,/ } > "$O/py_$nb.log" 2>&1 || { tail -30 "$O/py_$nb.log"; exit 1; }
+      tail -60 "$O/py_$nb.log" ;;
     resources)
       /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c blt_amd/csrc/bpe_kernels.hip -o /tmp/rk.o \
         -Rpass-analysis=kernel-resource-usage > "$O/resources.txt" 2>&1
