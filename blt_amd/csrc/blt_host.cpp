@@ -890,9 +890,18 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         const uint32_t k_last = h->chain_depth - 1;
         for (; k <= k_last; ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
-            if (finish_now(k))
+            if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
+                if (out_tokens) {
+                    // a caller that waits anyway: see whether the finish ran (its gate word, the longest
+                    // chunk, fit in LDS) before enqueueing the passes it turned into no-ops
+                    uint32_t lmax = 0;
+                    HIP_TRY(hipMemcpyAsync(&lmax, ws + L.total + 32, sizeof lmax, hipMemcpyDeviceToHost, s));
+                    HIP_TRY(hipStreamSynchronize(s));
+                    if (lmax <= blt::kFinCapTokens) break;
+                }
+            }
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
                                   false, &c, scan))
