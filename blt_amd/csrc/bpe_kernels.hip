@@ -826,6 +826,13 @@ constexpr int kStageWave = BLT_STAGE_WAVE;    // the LDS the table leaves, share
 #define BLT_LBWIN 1
 #endif
 constexpr int kLbWin = BLT_LBWIN;
+// Phase-1 instruction grouping (experiment switches; 0: the compiler's schedule).
+#ifndef BLT_TOKSCHED
+#define BLT_TOKSCHED 0
+#endif
+#ifndef BLT_P1SCHED
+#define BLT_P1SCHED 0
+#endif
 // Look-backs publish the inclusive prefixes of the tiles they fold (win_upgrade).
 #ifndef BLT_LB_UPGRADE
 #define BLT_LB_UPGRADE 1
@@ -1046,6 +1053,21 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         if (allm) m32 = 0x7FFF7FFFu;
         m[j] = (m32 & 0xFFFFu) | (m32 >> 15);
     }
+#if BLT_P1SCHED == 1
+    // experiment: both sub-tiles' addresses and table reads first (16 reads in flight per sub-tile)
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 33, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+    }
+#elif BLT_P1SCHED == 2
+    // experiment: reads in groups of 8, each behind the 16 address ops it needs
+#pragma unroll
+    for (int q = 0; q < 2 * kS; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 17, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+    }
+#endif
     // buffer end and chunk ends (uniform per wave range; rare)
     uint32_t bnext = ti.bge;   // first chunk start > the wave range's first position
 #pragma unroll
@@ -2061,6 +2083,12 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
         const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
         r[k] = tok_get<kHash>(p, tab, key);
     }
+#if BLT_TOKSCHED
+    if constexpr (kHash == 2) {   // experiment: the keys and bucket addresses, then all 16 bucket reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 56, 1);
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 1);
+    }
+#endif
     uint32_t racc = 0;
 #pragma unroll
     for (int k = 0; k < 16; k += 2) racc |= r[k] | r[k + 1];

@@ -10,6 +10,7 @@
 #   smoke              __graft_entry__.smoke(), smoke.log
 #   bench              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5, bench.json
 #   bench:ARGS         bench.py with extra arguments (commas for spaces), bench_<n>.json
+#   benchlib:LIBTAG:ARGS  bench.py on build/exp/libblt_bpe_LIBTAG.so
 #   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/exp/libblt_bpe_LIBTAG.so)
 #   tim:LIBTAG[:ARGS]  tools/tile_timing.py on a timing build (build/exp/libblt_bpe_LIBTAG.so)
 #   prof:WL            rocprofv3 --kernel-trace --stats of bench.py --workload WL (cfg2|cfg3|cfg5)
@@ -48,6 +49,11 @@ for st in "$@"; do
         timeout -k 10 400 python bench.py ${a//,/ } > "$O/bench_$nb.json" 2> "$O/bench_$nb.err"
         python tools/summarize_bench.py "$O/bench_$nb.json"
       fi ;;
+    benchlib)
+      # bench.py on an experiment build: benchlib:LIBTAG:ARGS (ARGS commas for spaces)
+      nb=$((nb + 1))
+      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 400 python bench.py ${b//,/ } > "$O/bench_${a}_$nb.json" 2> "$O/bench_${a}_$nb.err"
+      echo "[$a]"; python tools/summarize_bench.py "$O/bench_${a}_$nb.json" ;;
     kbench)
       lib=""; [ -n "$a" ] && lib="$R/build/exp/libblt_bpe_$a.so"
       BLT_LIB_PATH=$lib timeout -k 10 300 python tools/kbench.py --check >> "$O/kbench.jsonl" 2> "$O/kbench.err"
