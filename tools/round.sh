@@ -9,7 +9,7 @@
 #   tests              pytest -m gpu (every parity test), tests.log
 #   smoke              __graft_entry__.smoke(), smoke.log
 #   bench              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5, bench.json
-#   bench:ARGS         bench.py with extra arguments (commas for spaces), bench_<n>.json
+#   bench:ARGS         bench.py with extra arguments (+ for spaces), bench_<n>.json
 #   benchlib:LIBTAG:ARGS  bench.py on build/exp/libblt_bpe_LIBTAG.so
 #   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/exp/libblt_bpe_LIBTAG.so)
 #   tim:LIBTAG[:ARGS]  tools/tile_timing.py on a timing build (build/exp/libblt_bpe_LIBTAG.so)
@@ -46,22 +46,22 @@ for st in "$@"; do
         python tools/summarize_bench.py "$O/bench.json"
       else
         nb=$((nb + 1))
-        timeout -k 10 400 python bench.py ${a//,/ } > "$O/bench_$nb.json" 2> "$O/bench_$nb.err"
+        timeout -k 10 400 python bench.py ${a//+/ } > "$O/bench_$nb.json" 2> "$O/bench_$nb.err"
         python tools/summarize_bench.py "$O/bench_$nb.json"
       fi ;;
     benchlib)
-      # bench.py on an experiment build: benchlib:LIBTAG:ARGS (ARGS commas for spaces)
+      # bench.py on an experiment build: benchlib:LIBTAG:ARGS (ARGS + for spaces)
       nb=$((nb + 1))
-      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 400 python bench.py ${b//,/ } > "$O/bench_${a}_$nb.json" 2> "$O/bench_${a}_$nb.err"
+      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 400 python bench.py ${b//+/ } > "$O/bench_${a}_$nb.json" 2> "$O/bench_${a}_$nb.err"
       echo "[$a]"; python tools/summarize_bench.py "$O/bench_${a}_$nb.json" ;;
     kbench)
       lib=""; [ -n "$a" ] && lib="$R/build/exp/libblt_bpe_$a.so"
       BLT_LIB_PATH=$lib timeout -k 10 300 python tools/kbench.py --check >> "$O/kbench.jsonl" 2> "$O/kbench.err"
       tail -3 "$O/kbench.jsonl" ;;
     tim)
-      # per-wave phase timing of a timing build (-DBLT_TIMING): tim:LIBTAG[:ARGS] (ARGS commas for spaces)
+      # per-wave phase timing of a timing build (-DBLT_TIMING): tim:LIBTAG[:ARGS] (ARGS + for spaces)
       nb=$((nb + 1))
-      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 300 python tools/tile_timing.py ${b//,/ } \
+      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 300 python tools/tile_timing.py ${b//+/ } \
         > "$O/tim_${a}_$nb.txt" 2>&1
       head -22 "$O/tim_${a}_$nb.txt" | grep -E "^256|exit|publishes|wave  0|wave  8|wave 12|spins|rounds" ;;
     prof)
@@ -91,9 +91,9 @@ for st in "$@"; do
       timeout -k 10 300 python tools/cli_phases.py --out "$O/cli_phases_$nb.json" ${a:+--env "$a"} > "$O/cli_$nb.log" 2>&1
       python -c "import json;d=json.load(open('$O/cli_phases_$nb.json'));print(d.get('hip_init_probe'));[print(r['wall_s'],r['GBps']) for r in d['runs']]" ;;
     py)
-      # any tool script: py:tools/x.py[:ARGS] (ARGS commas for spaces), output py_<n>.log
+      # any tool script: py:tools/x.py[:ARGS] (ARGS + for spaces), output py_<n>.log
       nb=$((nb + 1))
-      timeout -k 10 300 python -u "$a" ${b//,/ } > "$O/py_$nb.log" 2>&1 || { tail -30 "$O/py_$nb.log"; exit 1; }
+      timeout -k 10 300 python -u "$a" ${b//+/ } > "$O/py_$nb.log" 2>&1 || { tail -30 "$O/py_$nb.log"; exit 1; }
       tail -60 "$O/py_$nb.log" ;;
     resources)
       /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c blt_amd/csrc/bpe_kernels.hip -o /tmp/rk.o \
