@@ -98,6 +98,7 @@ _DEBUG_SIGNATURES = {
     "blt_debug_byte_mode": (ctypes.c_int, [_vp]),
     "blt_debug_chain_depth": (ctypes.c_uint32, [_vp]),
     "blt_debug_set_finish": (ctypes.c_int, [ctypes.c_int]),
+    "blt_debug_set_chain": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_available_cpus": (ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint64]),
 }
 

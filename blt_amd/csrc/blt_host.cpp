@@ -577,7 +577,7 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
-    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, bytes, zero_bytes;
+    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, stat2, pctr, bytes, zero_bytes;
 };
 // Chain block of a general map (right after pass 1's status words): u64 pass totals [2], u32 done
 // word, u32 fused-fail word, u64 final total, u32 finish-gate word, pad.
@@ -602,7 +602,9 @@ WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
     L.gstat = L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));   // finish: a status word per group
-    L.bytes = single_pass ? L.cmap : L.gstat + up16(8 * L.nchunks);
+    L.stat2 = L.gstat + up16(8 * L.nchunks);   // chain launches: the second status area, per token tile
+    L.pctr = L.stat2 + up16(8 * L.ntiles);     // chain launches: ticket and emitted counters per pass
+    L.bytes = single_pass ? L.cmap : L.pctr + 8ull * blt::kChainMaxPasses;
     return L;
 }
 
@@ -694,6 +696,45 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }
+
+// u16 passes k .. k + np - 1 of a general map in one launch (blt::launch_scan_chain), as np
+// run_pass calls on the scan kernel would run them: tokens in place in d_out, chunk starts from
+// off_in (then the arrays alternate), totals tot[k & 1], tot[(k + 1) & 1], ...
+int run_chain(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
+              uint8_t* d_out, uint64_t n, uint32_t k, uint32_t np, const uint64_t* off_in, uint64_t* off_out,
+              uint64_t* tot, uint32_t* done) {
+    blt::PassParams p{};
+    p.in = d_out;
+    p.n = n;
+    p.cstart = off_in;
+    p.nchunks = L.nchunks;
+    p.out = d_out;
+    p.out_cap = 2 * n;
+    p.chunk_off = off_out;
+    p.status = reinterpret_cast<uint64_t*>(ws + L.status);
+    p.status2 = reinterpret_cast<uint64_t*>(ws + L.stat2);
+    p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
+    p.pass_ctr = reinterpret_cast<uint32_t*>(ws + L.pctr);
+    p.npasses = np;
+    p.n_dev = tot + ((k - 1) & 1);
+    p.total = tot + (k & 1);
+    p.done = done;
+    p.pass_id = k;
+    p.ntiles = (uint32_t)((n + blt::kTilePosTok - 1) / blt::kTilePosTok);
+    p.hbuckets = t->hbuckets;
+    p.hmul1 = h->hmul1;
+    p.hmul2 = h->hmul2;
+    p.hshift = h->hshift;
+    p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
+    p.hone = h->hone ? 1u : 0u;
+    p.sticky = h->sticky.load(std::memory_order_acquire);
+    p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
+    HIP_TRY(blt::launch_scan_chain(p, dev, s));
+    return 0;
+}
+
+// Test hook (blt_debug_set_chain): 0 runs every u16 pass as its own launch.
+std::atomic<int> g_chain{1};
 
 // Passes 1 and 2 of a general map in one launch (blt::launch_scan_fused): bytes d_in to the second
 // pass's tokens in d_out, its total, chunk offsets and done word as u16 pass 1's.
@@ -882,6 +923,19 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         fin_tried = true;
         return true;
     };
+    // passes from k on that one chain launch can run (at most lim): scan-kernel passes (every chunk
+    // at least kTokRange tokens), none of them the finish kernels' pass; 0 or 1: separate launches
+    const bool chain_ok = g_chain.load(std::memory_order_relaxed) && L.nchunks <= blt::kChainMaxChunks &&
+                          n < (1ull << 31);   // (token positions in 32 bits in the chain kernel)
+    auto chain_len = [&](uint64_t k0, uint64_t lim) {
+        uint64_t np = 0;
+        if (!chain_ok) return np;
+        for (uint64_t kk = k0; np < lim && np < blt::kChainMaxPasses; ++kk, ++np) {
+            if (kk >= 64 || (cs >> kk) < blt::kTokRange) break;
+            if (!fin_tried && (cs >> kk) <= blt::kFinCapTokens) break;
+        }
+        return np;
+    };
     if (bounded) {
         // a bounded chain (no value can be made from itself): u16 passes 1 .. depth - 1 are all a
         // pass can need, enqueued without reading the device's pass count; passes after the one
@@ -889,6 +943,14 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         // and chunk offsets.  Only a caller asking for the token count waits (once).
         const uint32_t k_last = h->chain_depth - 1;
         for (; k <= k_last; ++k) {
+            if (const uint64_t np = chain_len(k, k_last - k + 1); np >= 2) {
+                if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
+                                       tot, done))
+                    return rc;
+                cur ^= (int)(np & 1);
+                k += np - 1;
+                continue;
+            }
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
@@ -922,6 +984,15 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     }
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
+            if (const uint64_t np = chain_len(k, (uint64_t)(batch - b)); np >= 2) {
+                if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
+                                       tot, done))
+                    return rc;
+                cur ^= (int)(np & 1);
+                k += np - 1;
+                b += (int)np - 1;
+                continue;
+            }
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             if (finish_now(k))
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
@@ -1531,6 +1602,7 @@ int blt_debug_byte_mode(const blt_bpe* h) {
 // Not in the public header (tests): 0 disables the finish kernels of a general map's chain, 1 (the
 // default) enables them; returns the previous setting.
 int blt_debug_set_finish(int on) { return g_finish.exchange(on ? 1 : 0); }
+int blt_debug_set_chain(int on) { return g_chain.exchange(on ? 1 : 0); }
 
 // Not in the public header: a general map's longest merge chain (0: single-pass, or unbounded).
 uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0; }

@@ -235,18 +235,29 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
 // the windowed path (one inode lock, ~5.5 GB/s on tmpfs) becomes the runtime's device-to-host
 // copies into pages the preallocation below already holds.  Returns 1 (nothing done) when the
 // file cannot be sized or mapped, so the caller takes the windowed path.
+struct OutMap {
+    uint8_t* m = nullptr;   // shared mapping of the output file, `total` bytes
+    size_t total = 0;
+    bool sized = false;     // the file was ftruncate'd to total (undone when the mapping failed)
+    bool registered = false;
+};
+
+// The output file sized to its bound and mapped, its first `est` bytes' pages allocated
+// (preallocate) and mapped writable (MADV_POPULATE_WRITE, several threads): on a helper thread while
+// the HIP runtime starts, so the device-to-host copies of the run land in pages that are already
+// there.  (Page faults under the copies, one per 4 KiB page, were most of the CLI's tokenise phase.)
+void map_output(int fd, size_t total, size_t est, OutMap* om);
+
 int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, int fd, size_t head,
-                    const uint8_t* head_bytes) {
+                    const uint8_t* head_bytes, const OutMap& om) {
     const size_t cap = st.kind == Strategy::kPassthrough ? n : 2 * n;
     const size_t total = head + cap;
     if (total == 0) return 0;
-    if (ftruncate(fd, (off_t)total) != 0) return 1;
-    void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    if (m == MAP_FAILED) {
-        (void)ftruncate(fd, 0);
+    if (!om.m || om.total != total) {
+        if (om.sized) (void)ftruncate(fd, 0);
         return 1;
     }
-    uint8_t* out = static_cast<uint8_t*>(m);
+    uint8_t* out = om.m;
     if (head) memcpy(out, head_bytes, head);
     size_t olen = 0;
     int rc = 0;
@@ -267,7 +278,8 @@ int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, 
             olen += w;
         }
     }
-    munmap(m, total);
+    if (om.registered) (void)hipHostUnregister(om.m);
+    munmap(om.m, total);
     const std::string msg = rc ? last_error() : std::string();
     // the bytes produced (an error leaves the content token only, like a run that wrote no chunk)
     if (ftruncate(fd, (off_t)(head + (rc ? 0 : olen))) != 0 && !rc) return os_error(errno);
@@ -283,6 +295,40 @@ void preallocate(int fd, size_t bytes) {
     constexpr size_t kStep = size_t(64) << 20;
     for (size_t off = 0; off < bytes; off += kStep)
         if (fallocate(fd, FALLOC_FL_KEEP_SIZE, (off_t)off, (off_t)std::min(kStep, bytes - off)) != 0) return;
+}
+
+bool env_on(const char* name, bool dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? strcmp(v, "0") != 0 : dflt;
+}
+
+void map_output(int fd, size_t total, size_t est, OutMap* om) {
+    if (ftruncate(fd, (off_t)total) != 0) return;
+    om->sized = true;
+    preallocate(fd, std::min(est, total));
+    void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) return;
+    om->m = static_cast<uint8_t*>(m);
+    om->total = total;
+    if (env_on("BLT_OUT_POPULATE", true)) {   // (env: A/B runs)
+        // 2 MiB-aligned pieces over 4 threads; best effort (older kernels: EINVAL, the copies fault)
+        constexpr size_t kPiece = size_t(2) << 20;
+        const size_t len = std::min(est, total);
+        const size_t pieces = (len + kPiece - 1) / kPiece;
+        auto part = [&](size_t t, size_t nt) {
+            for (size_t i = t; i < pieces; i += nt) {
+                const size_t off = i * kPiece;
+                if (madvise(om->m + off, std::min(kPiece, len - off), MADV_POPULATE_WRITE) != 0) return;
+            }
+        };
+        std::thread th[3];
+        for (size_t t = 0; t < 3; ++t) th[t] = std::thread(part, t + 1, size_t(4));
+        part(0, 4);
+        for (auto& t : th) t.join();
+    }
+    // (env experiment) the whole mapping page-locked for the runtime's copies
+    if (env_on("BLT_OUT_REGISTER", false))
+        om->registered = hipHostRegister(om->m, total, hipHostRegisterDefault) == hipSuccess;
 }
 
 // Stream path (pipeline.rs:196-433): one read per chunk, at most `threads` chunks in flight, a
@@ -503,14 +549,29 @@ int run(const blt_run_config* c) {
         direct = fstat(ofd, &ob) == 0 && S_ISREG(ob.st_mode);
     }
     std::thread prealloc;
+    OutMap om;
     if (direct && n) {
         // expected output: basic 2 bytes per byte; BPE about 1 (large merge maps: ~0.5 tokens per byte)
         const size_t est = head + (st.kind == Strategy::kBasic ? 2 * n : n);
-        prealloc = std::thread([ofd, est] { preallocate(ofd, est); });
+        const size_t total = head + (st.kind == Strategy::kPassthrough ? n : 2 * n);
+        prealloc = std::thread([ofd, total, est, &om] { map_output(ofd, total, est, &om); });
     }
+    // (env experiment) the input mapping page-locked for the runtime's copies, beside the device setup
+    bool in_registered = false;
+    std::thread reg_in;
+    if (map && st.kind == Strategy::kBpe && env_on("BLT_IN_REGISTER", false))
+        reg_in = std::thread([map, n, &in_registered] {
+            in_registered = hipHostRegister(const_cast<uint8_t*>(map), n, hipHostRegisterReadOnly) == hipSuccess;
+        });
     if (prewarm.joinable()) prewarm.join();
     else if (st.kind == Strategy::kBpe) st.gpus = gpu_count(st.gpus);
     if (prealloc.joinable()) prealloc.join();
+    if (reg_in.joinable()) reg_in.join();
+    struct Unregister {
+        const uint8_t* p;
+        bool on;
+        ~Unregister() { if (on) (void)hipHostUnregister(const_cast<uint8_t*>(p)); }
+    } unregister{map, in_registered};
     if (timing) {
         timespec t;
         clock_gettime(CLOCK_MONOTONIC, &t);
@@ -533,7 +594,7 @@ int run(const blt_run_config* c) {
     int rc = 0;
     const uint8_t tok[2] = {(uint8_t)(c->content_token >> 8), (uint8_t)c->content_token};
     int drc = 1;
-    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok);
+    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om);
     if (drc <= 0) {
         rc = drc;
     } else {

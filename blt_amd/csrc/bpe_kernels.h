@@ -69,6 +69,10 @@ struct PassParams {
                                // refuse (error bit 32, no output) when ntiles > ctl[kCtlCover]
     uint32_t* fused_fail;      // fused passes 1 + 2: set to 1 when a wave range's halo holds no
                                // restart (the host then runs the two-kernel chain instead)
+    uint64_t* status2;         // chain launches: the second status area (passes alternate; [ntiles])
+    uint32_t* pass_ctr;        // chain launches: per pass [2 i] tile ticket, [2 i + 1] tiles emitted;
+                               // zeroed by the chunk-map kernel ahead of the launch
+    uint32_t npasses;          // chain launches: u16 passes pass_id .. pass_id + npasses - 1
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
@@ -90,6 +94,14 @@ constexpr uint32_t kDoneBytePass = 0x80000000u;
 // p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
 // at least kTokRange tokens.
 hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
+// u16 passes p.pass_id .. p.pass_id + p.npasses - 1 of a general map in one launch
+// (seg::scan_tokens_kernel<kHash, false, true>), each as launch_scan_tokens would run it: the first
+// pass's chunk map kernel (which also zeroes p.pass_ctr), then one persistent launch whose passes
+// meet at a counter of emitted tiles.  Needs p.nchunks <= kChainMaxChunks (chunk starts in LDS),
+// every chunk at least kTokRange tokens in every pass, and p.status2 beside p.status.
+hipError_t launch_scan_chain(const PassParams& p, int device, hipStream_t s);
+constexpr uint64_t kChainMaxChunks = 1024;
+constexpr uint32_t kChainMaxPasses = 64;
 // Passes 1 and 2 of a general map in one kernel (seg::scan_tokens_kernel<kHash, true>): bytes in,
 // the second pass's big-endian tokens out, for maps whose bucket table fits in LDS and chunk sizes
 // >= kMinChunkBytes.  A wave range takes the first pass's carry-in from the 64 bytes before it

@@ -228,8 +228,17 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 // but still count themselves out, so the self-reset zeroes its ntiles words as usual.  The word is
 // read at the workgroup's start (a scalar load, written before the launch on its stream) and tested
 // after the table copy, off the critical path.
+#ifndef BLT_COVER_LOAD
+#define BLT_COVER_LOAD 0
+#endif
 __device__ __forceinline__ uint32_t ws_cover(const PassParams& p) {
+#ifdef BLT_WS_NOCHECK   // (experiment: no coverage check)
+    return 0xFFFFFFFFu;
+#elif BLT_COVER_LOAD == 0
     return p.ws_check ? *(const volatile uint32_t*)(p.ctl + kCtlCover) : 0xFFFFFFFFu;
+#else
+    return p.ws_check ? __hip_atomic_load(p.ctl + kCtlCover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xFFFFFFFFu;
+#endif
 }
 __device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles, uint32_t cover) {
     if (ntiles <= cover) return false;
@@ -1381,6 +1390,8 @@ __device__ __forceinline__ u32x4 block_of(const u32x4& a, const u32x4& b, uint32
 // (rg = 0: every tile of a dense text emits a multiple of 8 tokens) that is the whole emission;
 // otherwise lane 0 stores the head of its block (its first 8 - rg/2 tokens) and lane 63 the block
 // after the range (its last rg/2 tokens) token by token.
+// kPol / kPol16: cache policy of the 16-byte and the 2-byte stores (chain launches: sc1, 16)
+template <int kPol = BLT_STPOL, int kPol16 = 0>
 __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, uint32_t rg, __amdgpu_buffer_rsrc_t ro,
                                            uint32_t ab, int lane) {
     const uint32_t sel = c ? 0x05040100u : 0x07060302u;   // low halves (c = 1) or high halves (c = 0)
@@ -1389,7 +1400,7 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
     const uint32_t o = ab + 16u * (uint32_t)lane;
     if (rg == 0) {
-        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, BLT_STPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, kPol);
         return;
     }
     u32x4 Q;   // lane l - 1's tokens
@@ -1397,15 +1408,15 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q)
         Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
     const uint32_t off = 16u - rg;
-    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, BLT_STPOL);
+    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, kPol);
     if (lane == 0 || lane == 63) {
         const uint32_t h = 8u - (rg >> 1);   // tokens of this lane in its own block
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint16_t tok = (uint16_t)(P[k >> 1] >> (16 * (k & 1)));
-            if (lane == 0 && (uint32_t)k < h) __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, 0);
+            if (lane == 0 && (uint32_t)k < h) __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, kPol16);
             if (lane == 63 && (uint32_t)k >= h)
-                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 1024u + 2u * (k - h)), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 1024u + 2u * (k - h)), 0, kPol16);
         }
     }
 }
@@ -1512,7 +1523,7 @@ __device__ __forceinline__ void copy_read_pad(const uint8_t* arr, uint32_t x0, c
     }
     d.vf = bf ? *reinterpret_cast<const uint16_t*>(arr + stage_phys(x0 + of)) : (uint16_t)0;
 }
-template <int NB, bool kOob = BLT_OOB_COPY != 0>
+template <int NB, bool kOob = BLT_OOB_COPY != 0, int kPol = BLT_STPOL, int kPol16 = 0>
 __device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const CopyPart& c, int lane, const CopyData<NB>& d) {
     const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
     const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
@@ -1523,16 +1534,16 @@ __device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const Copy
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             const uint32_t o = (uint32_t)lane + 64u * q < nfull ? c.abp + hend + 16u * lane + 1024u * q : kOobOff;
-            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)o, 0, BLT_STPOL);
+            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)o, 0, kPol);
         }
-        __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(bf ? c.abp + of : kOobOff), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(bf ? c.abp + of : kOobOff), 0, kPol16);
         return;
     }
 #pragma unroll
     for (int q = 0; q < NB; ++q)
         if ((uint32_t)lane + 64u * q < nfull)
-            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, BLT_STPOL);
-    if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, kPol);
+    if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, kPol16);
 }
 
 // Sparse wave range: per-lane landing mask and token offset, the range's token count.
@@ -1733,7 +1744,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
     const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
+#if BLT_COVER_LOAD != 2
     const uint32_t cover = ws_cover(p);
+#endif
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
     if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
@@ -1768,6 +1781,9 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     uint32_t T = uni(s_tk[kRing - 2]);    // tile in phase 1
     uint32_t Tp = kNone;                  // tile waiting for emission
     uint32_t Tq = uni(s_tk[kRing - 1]);   // the tile after T (its bytes load during T's iteration)
+#if BLT_COVER_LOAD == 2
+    const uint32_t cover = ws_cover(p);
+#endif
     if (ws_refused(p, ntiles, cover)) T = kNone;   // (its two tickets are dropped: the reset zeroes them)
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     TInfo ti = {}, tip = {};
@@ -1977,23 +1993,15 @@ __device__ __forceinline__ bool pass_done(const PassParams& p) {
 // the scan's ticket and status words (one per kTileTok tokens, so the wave ranges cover them): the
 // previous pass has finished with them.  The error flags and first-error record (ctl[1..]) stay,
 // so the host reports the chain's first failure (the chain's first memset zeroed them).
-__global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
-    if (pass_done(p)) return;
-    const uint64_t n = token_count(p);
-    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
-    if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
-    const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
-    if (lo >= n) return;
-    const uint64_t* cs = p.cstart;
-    const uint64_t nc = p.nchunks;
+// Chunk-map word of the wave range [lo, hi) from the sorted chunk starts cs[0, nc): lower bound
+// of lo, the start inside the range and the end (a start minus one) inside it.
+__device__ __forceinline__ uint64_t cm_word(const uint64_t* cs, uint64_t nc, uint64_t lo, uint64_t hi, bool& bad) {
     uint64_t a = 0, b = nc;
     while (a < b) {
         const uint64_t mid = (a + b) >> 1;
         if (cs[mid] < lo) a = mid + 1; else b = mid;
     }
     uint64_t w = 0;
-    bool bad = false;
     if (a < nc && cs[a] < hi) {
         w |= (cs[a] - lo) | kCmStart | (a << 32);
         bad |= a + 1 < nc && cs[a + 1] < hi;
@@ -2003,6 +2011,33 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
         w |= ((cs[e] - 1 - lo) << 12) | kCmEnd;
         bad |= e + 1 < nc && cs[e + 1] <= hi;
     }
+    return w;
+}
+
+// A map of at most kCmLds chunks is searched in LDS: the block loads every chunk start in one
+// round of parallel loads instead of a binary search's log2(nchunks) dependent ones (the kernel
+// runs before every u16 pass, and a deep chain's late passes are made of such round trips).
+constexpr uint32_t kCmLds = 1024;
+__global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
+    __shared__ uint64_t s_cs[kCmLds];
+    const bool done = pass_done(p);      // (both loads in flight together)
+    const uint64_t n = token_count(p);
+    if (done) return;
+    const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
+    if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
+    if (p.pass_ctr && r < 2u * p.npasses) p.pass_ctr[r] = 0u;   // a chain launch's counters
+    const uint64_t nc = p.nchunks;
+    const bool in_lds = nc <= kCmLds;
+    if ((uint64_t)blockIdx.x * 256u * kWavePos >= n) return;   // uniform: no range of this block is live
+    if (in_lds) {
+        for (uint32_t i = threadIdx.x; i < nc; i += 256u) s_cs[i] = p.cstart[i];
+        __syncthreads();
+    }
+    const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
+    if (lo >= n) return;
+    bool bad = false;
+    const uint64_t w = in_lds ? cm_word(s_cs, nc, lo, hi, bad) : cm_word(p.cstart, nc, lo, hi, bad);
     if (bad) flag_error(p.ctl, KARG(sticky), 16u);   // chunks shorter than a wave range: host bug
     p.cmap[r] = w;
 }
@@ -2010,8 +2045,12 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
 // Tokens of tile Tn into x (the same straight-line loads as load_tile; near the buffer end the
 // lanes' tokens again one by one), and each wave range's chunk-map word (0 past the end).
 // Sub-tile j of wave w: tokens [j kSubTok + 1024 w, +1024), wave range Tn kGroupsTok + j kWaves + w.
+// kChain (chain launches): every load sc1 (the tokens were written by this launch's previous pass,
+// write-through), and no chunk-map words (the caller derives them from the chunk starts in LDS).
+template <bool kChain = false>
 __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32_t Tn, uint32_t wave, int lane,
                                          uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2]) {
+    constexpr int kPol = kChain ? 16 : BLT_LDPOL, kPol2 = kChain ? 16 : 0;
     const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
     const uint64_t tile0 = (uint64_t)Tn * kTileTok;
     const uint64_t left = n > tile0 ? n - tile0 : 0;
@@ -2022,13 +2061,15 @@ __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32
     for (int j = 0; j < kSt; ++j) {
         const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
         const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
-        const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, BLT_LDPOL);
-        const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, BLT_LDPOL);
+        const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, kPol);
+        const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, kPol);
         x[j][0] = v0[0]; x[j][1] = v0[1]; x[j][2] = v0[2]; x[j][3] = v0[3];
         x[j][4] = v1[0]; x[j][5] = v1[1]; x[j][6] = v1[2]; x[j][7] = v1[3];
-        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, 0);
-        const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * ((uint32_t)j * kWaves + wave)), 0, 0);
-        cw[j][0] = c[0]; cw[j][1] = c[1];
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, kPol2);
+        if constexpr (!kChain) {
+            const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * ((uint32_t)j * kWaves + wave)), 0, 0);
+            cw[j][0] = c[0]; cw[j][1] = c[1];
+        }
     }
     const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
 #pragma unroll
@@ -2037,11 +2078,11 @@ __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32
         if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
             const __amdgpu_buffer_rsrc_t r = rsrc_at(in + 2 * tile0, 2 * left);
             const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
-            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, 0);
+            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, kPol2);
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                x[j][q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, 0) |
-                          ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, 0) << 16);
+                x[j][q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, kPol2) |
+                          ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, kPol2) << 16);
         }
     }
 }
@@ -2149,10 +2190,17 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
 
 // Emission of sub-tile j's wave range (as emit_tile), its chunk start from the chunk-map word.
 // rem: tokens from the range start to the buffer end; wtok: the range's first input token.
+// kChain (chain launches): every store sc1 (write-through: the next pass of the same launch reads
+// them on any XCD) and the chunk offsets from p (they alternate between passes).
+__device__ __forceinline__ void coff_store(uint64_t* a, uint64_t v, bool sc1) {
+    if (sc1) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *a = v;
+}
+template <bool kChain = false>
 __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uint32_t rem, uint32_t cwl, uint32_t cwh,
                                          int lane, int j, const TileStateT<kSt>& st, const uint32_t* gin,
                                          uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave, bool has_coff,
-                                         bool inplace = true) {
+                                         bool inplace = true, uint64_t* coff_chain = nullptr) {
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
@@ -2163,8 +2211,8 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const bool cstart = has_coff && (cwl & kCmStart) != 0u;
     if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
         // dense: every pair merges, so the only possible chunk start is the range's first token
-        if (cstart && lane == 0) KARG(chunk_off)[cwh] = O + goff;
-        emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
+        if (cstart && lane == 0) coff_store((kChain ? coff_chain : KARG(chunk_off)) + cwh, O + goff, kChain);
+        emit_dense<kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
     }
     const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
@@ -2177,7 +2225,9 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
     if (cstart) {
         const uint32_t e = (cwl & 0x7FFu) - 16u * (uint32_t)lane;
-        if (e < 16u) KARG(chunk_off)[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+        if (e < 16u)
+            coff_store((kChain ? coff_chain : KARG(chunk_off)) + cwh, O + goff + lane_off + __popc(L & ((1u << e) - 1u)),
+                       kChain);
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
@@ -2188,7 +2238,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const CopyPart cp = {gb & ~15u, gb & 15u, (gb & 15u) + 2u * wcnt};
     CopyData<kCopyBlkTok> d;
     copy_read_pad(stg, x0, cp, lane, d);
-    copy_store<kCopyBlkTok, false>(ro, cp, lane, d);   // (branch-free here: f2 +2.5 %)
+    copy_store<kCopyBlkTok, false, kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(ro, cp, lane, d);   // (branch-free here: f2 +2.5 %)
 }
 
 // ===========================================================================================
@@ -2417,8 +2467,51 @@ __device__ __forceinline__ void fused_front(const PassParams& p, uint32_t tab, u
     }
 }
 
-template <int kHash, bool kFused = false>
+// Chunk-map words of a chain launch (no chunk_map_kernel between its passes): the wave range at
+// token lo from the pass's chunk starts in LDS (cs[0, nc), nc <= kCmLds; positions below 2^32, which
+// the host checks), the lower bound found by two ballots (blocks of 16 starts, then inside the
+// block) instead of a dependent search.  The same word as chunk_map_kernel's cm_word.
+__device__ __forceinline__ void lds_cm_word(const uint32_t* cs, uint32_t nc, uint32_t lo, int lane, uint32_t (&cw)[2],
+                                            bool& bad) {
+    const uint32_t i1 = (uint32_t)lane * 16u;
+    const uint32_t nb = __popcll(__ballot(i1 < nc && cs[i1 < nc ? i1 : 0u] < lo));   // blocks starting below lo
+    uint32_t a = 0;
+    if (nb != 0) {
+        const uint32_t base = (nb - 1u) * 16u, i2 = base + (uint32_t)lane;
+        a = base + __popcll(__ballot(lane < 16 && i2 < nc && cs[i2 < nc ? i2 : 0u] < lo));
+    }
+    a = uni(a);
+    const uint32_t hi = lo + (uint32_t)kWavePos;
+    uint32_t wl = 0, wh = 0;
+    const uint32_t ca = a < nc ? cs[a] : 0xFFFFFFFFu;
+    if (ca < hi) {
+        wl |= (ca - lo) | kCmStart;
+        wh = a;
+        bad |= a + 1u < nc && cs[a + 1u] < hi;
+    }
+    const uint32_t e = (a < nc && ca == lo) ? a + 1u : a;   // first chunk start > lo
+    const uint32_t ce = e < nc ? cs[e] : 0xFFFFFFFFu;
+    if (ce <= hi && ce != 0xFFFFFFFFu) {
+        wl |= ((ce - 1u - lo) << 12) | kCmEnd;
+        bad |= e + 1u < nc && cs[e + 1u] <= hi;
+    }
+    cw[0] = wl;
+    cw[1] = wh;
+}
+
+// kChain: one launch runs u16 passes p.pass_id .. p.pass_id + p.npasses - 1 of a general map
+// (launch_scan_chain).  Between passes the workgroups wait until every tile of the pass is emitted
+// (a counter per pass; every workgroup waiting has claimed no tile of the pass, and every claimed
+// tile belongs to a running workgroup, so the wait ends whatever else runs on the device), then
+// read the pass's count and done word and take the next pass's tickets; the map's table stays in
+// LDS.  Token, chunk-offset and count stores are sc1 (write-through) and the next pass's loads sc1
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores drained by each wave's vmcnt(0),
+// then one agent-scope add per tile, sc1 loads).  The passes alternate status areas (each pass
+// zeroes the next pass's word of every tile it resolves), totals and chunk-offset arrays exactly as
+// separate launches do, so the chain's host side and chain_final_kernel read the same words.
+template <int kHash, bool kFused = false, bool kChain = false>
 __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
+    static_assert(!(kFused && kChain), "a chain launch runs u16 passes");
     constexpr bool kHashLds = kHash != 0;
     extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves * kStageTokPhys];   // padded
@@ -2430,14 +2523,19 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     __shared__ uint32_t s_tk[kRing];
     __shared__ uint32_t s_p1cnt[kRing];
     __shared__ uint32_t s_rdone, s_lbdone, s_tkdone;
+    __shared__ uint32_t s_cs[kChain ? kCmLds : 1];   // chain: the pass's chunk starts (below 2^32)
+    __shared__ uint32_t s_emc[kRing];                // chain: waves done with each iteration's stores
+    __shared__ uint32_t s_tk0[2];                    // chain: a pass's first two tickets
 
-    if (!kFused && pass_done(p)) return;   // an earlier pass merged nothing (uniform over the grid)
+    // an earlier pass merged nothing (uniform over the grid); both loads in flight together
+    const bool done = !kFused && pass_done(p);
+    uint64_t n = kFused ? p.n : uni64(token_count(p));   // fused: bytes
+    if (done) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = uni((uint32_t)tid >> 6);
-    const uint64_t n = kFused ? p.n : uni64(token_count(p));   // fused: bytes
     const bool has_coff = p.chunk_off != nullptr;
-    const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
+    uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
     // the grid was sized for the token bound; workgroups past the tiles the previous pass left leave
     // before copying the table (the ones below claim every ticket)
     if (blockIdx.x >= ntiles) return;
@@ -2463,201 +2561,303 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                     (__attribute__((address_space(3))) void*)(dst + u0), 16, 0, 0);
         }
     }
+    // ticket counter: the control block's, or a chain launch's per pass ([0] tickets, [1] tiles emitted)
+    // A chain launch's pass pi uses the kernel argument's arrays with the roles of each pair swapped
+    // when pi is odd (totals, chunk offsets, status areas; KARG reloads where used: nothing per pass
+    // is held in registers but pi and p.status, which the shared look-back helpers read).
+    uint32_t pi = 0;
+    auto sw = [&]() { return (pi & 1u) != 0u; };
+    auto tkp_of = [&]() { return kChain ? KARG(pass_ctr) + 2u * pi : p.ctl; };
+    uint32_t* tkp = tkp_of();
+    const uint32_t nc = kChain ? (uint32_t)p.nchunks : 0u;
+    // chain: the pass's chunk starts into LDS (sc1: the previous pass of this launch wrote them)
+    auto load_starts = [&]() {
+        const uint64_t* cst = sw() ? KARG(chunk_off) : KARG(cstart);
+        for (uint32_t i = (uint32_t)tid; i < nc; i += (uint32_t)kThreads)
+            s_cs[i] = (uint32_t)__hip_atomic_load(const_cast<uint64_t*>(cst) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     if (tid == 0) {
-        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);
-        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);
-        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
+        s_tk0[0] = atomicAdd(tkp, 1u);
+        s_tk0[1] = atomicAdd(tkp, 1u);
+        for (int r = 0; r < kRing; ++r) { s_p1cnt[r] = 0; s_emc[r] = 0; }
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
+    if constexpr (kChain) load_starts();
     __syncthreads();
     const uint32_t tab = kHashLds ? uni(lds_addr(s_tokhash)) : 0u;
-    uint32_t T = uni(s_tk[kRing - 2]);
+    uint32_t T = uni(s_tk0[0]);
     uint32_t Tp = kNone;
-    uint32_t Tq = uni(s_tk[kRing - 1]);
+    uint32_t Tq = uni(s_tk0[1]);
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     __syncthreads();
 
-    uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca[kSt][2], cb[kSt][2];
+    // chain: chunk-map words of tile Tn's wave ranges from the chunk starts in LDS
+    auto chain_map = [&](uint32_t Tn, uint32_t (&cw)[kSt][2]) {
+        bool bad = false;
 #pragma unroll
-    for (int j = 0; j < kSt; ++j) { na[j] = nb[j] = 0u; ca[j][0] = ca[j][1] = cb[j][0] = cb[j][1] = 0u; }
-    if (T < ntiles) {
-        if constexpr (kFused) load_fused(p, n, T, wave, lane, xa, na);
-        else load_tok(p, n, T, wave, lane, xa, na, ca);
-    }
-    TileStateT<kSt> sa, sb;
-    uint64_t lbs[kLbWin];
-    uint32_t it = 0;
-    uint32_t cwp[kSt][2];   // Tp's chunk-map words
-#pragma unroll
-    for (int j = 0; j < kSt; ++j) cwp[j][0] = cwp[j][1] = 0u;
-
-    auto step = [&](uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2], uint32_t (&xq)[kSt][8],
-                    uint32_t (&nxtq)[kSt], uint32_t (&cwq)[kSt][2], TileStateT<kSt>& sc, const TileStateT<kSt>& sp) {
-        const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
-        uint64_t stamp[7];
-        const bool stamping = kTiming && p.debug != nullptr;
-        if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map words have landed
-        if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-        uint32_t cwl[kSt], cwh[kSt];
-#pragma unroll
-        for (int j = 0; j < kSt; ++j) {
-            cwl[j] = kFused ? 0u : uni(cw[j][0]);   // fused: from the front end
-            cwh[j] = kFused ? 0u : uni(cw[j][1]);
-        }
-        if (Tq < ntiles) {
-            if constexpr (kFused) load_fused(p, n, Tq, wave, lane, xq, nxtq);
-            else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
-        }
-        uint32_t tk = kNone;
-        if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
-        asm volatile("" ::: "memory");
-
-        bool lbw = wave == 0;
-        if (T < ntiles) {
-            if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
-            uint32_t m[kSt], live = 0;
-            uint32_t rem2[kSt], C2[kSt];
-            bool nok[kSt];
-            if constexpr (kFused) {
-#pragma unroll
-                for (int j = 0; j < kSt; ++j)
-                    fused_front<kHash>(p, tab, x[j], nxt[j], (uint64_t)T * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos,
-                                       n, lane, wave, s_stage, rem2[j], nok[j], cwl[j], cwh[j], C2[j]);
-#pragma unroll
-                for (int j = 0; j < kSt; ++j)
-                    m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem2[j], cwl[j], lane, j, sc, live, nok[j]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < kSt; ++j)
-                    m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
-            }
-            const uint32_t wl = __ballot(live) != 0 ? 1u : 0u;
-            lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], wl);
-            if constexpr (kFused) {
-                // a fused range knows its carry-in (C2, from the halo): its wave function is the
-                // constant one, with the count under C2 and the carry into the next range (the
-                // range's tokens fill only its first rem2 positions, so the lane functions' own
-                // carry-out, past the unused positions, is not it)
-#pragma unroll
-                for (int j = 0; j < kSt; ++j) {
-                    uint32_t L2, M2, off2;
-                    lands1(m[j], sc.mv[j] >> 16, sc.ex[j], C2[j], L2, M2, off2);
-                    const uint32_t cnt = uni(lane_u32(off2 + __popc(L2), 63));
-                    uint32_t co = 1u;
-                    if (nok[j]) {
-                        const uint32_t last = (rem2[j] > kWavePos ? kWavePos : rem2[j]) - 1u;
-                        const uint32_t mb = uni(__builtin_amdgcn_readlane((int)M2, (int)(last >> 4)));
-                        co = ((mb >> (last & 15u)) & 1u) ? 0u : 1u;
-                    }
-                    if (lane == 63) {
-                        const uint32_t g = (uint32_t)j * kWaves + wave;
-                        s_wfn[slot][g][0] = wl << 1;
-                        s_wfn[slot][g][1] = co;
-                        s_wfn[slot][g][2] = cnt;
-                        s_wfn[slot][g][3] = cnt;
-                    }
-                }
-            }
-            __builtin_amdgcn_s_setprio(0);
-            uint32_t old = 0;
-            if (lane == 0)
-                old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            old = uni(old);
-            lbw = old == (uint32_t)kWaves * (it / kRing);
-            if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile<kGroupsTok, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
-                if (lane == 0) lds_release(&s_rdone, it + 1u);
-            }
-        }
-        if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
-
-        if (lbw && Tp < ntiles) {
-            uint32_t C = 1u, how = 0xFFFFu, spins = 0, live = 0;
-            uint64_t O = 0ull;
-            const bool lb = Tp > 0;
-            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
-            wait_ge(p, &s_rdone, it);
-            const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
-            const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live);
-            live |= (tfl >> 1) & 1u;   // tiles up to and including Tp
-            if (lane == 0) {
-                const uint64_t end = O + (C == 1u ? tf3 : tf2);
-                if (C > 1u || O > (uint64_t)Tp * kTileTok || end > n) {
-                    if (C <= 1u) record_error(p, 4u, Tp, 0xFFu, O, end, C);
-                    O = 0; C = 2u;
-                }
-                s_C[pslot] = C;
-                s_O[pslot] = O;
-                lds_release(&s_lbdone, it + 1u);
-                const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
-                if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
-                if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
-                if (Tp == ntiles - 1) {
-                    *KARG(total) = fin;
-                    if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
-                    // The fixpoint: this pass merged nothing, or none of its merges made a key
-                    // component, so the next pass merges nothing (a pair of two tokens this pass
-                    // left alone was looked up here and rejected; a new token is in no key).
-                    if (p.done && C <= 1u && (fin == n || !live)) *p.done = p.pass_id;
-                }
-                if (kDebugRecord && p.debug) {
-                    uint64_t* d = p.debug + 4ull * Tp;
-                    d[0] = O;
-                    d[1] = ((uint64_t)C << 32) | how;
-                    d[2] = ((uint64_t)tf3 << 32) | tf2;
-                    d[3] = ((uint64_t)tf1 << 32) | tf0;
-                }
-            }
-        }
-
-        if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
-        if (Tp < ntiles) {
-            wait_ge(p, &s_lbdone, it + 1u);
-            if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
-            if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
-            const uint32_t Cp = uni(s_C[pslot]);
-            if (Cp <= 1u) {
-                const uint64_t Op = uni64(s_O[pslot]);
-#pragma unroll
-                for (int j = 0; j < kSt; ++j) {
-                    const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
-                    emit_tok(p, wtok, kFused ? 0u : rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
-                             s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff, !kFused);
-                }
-            }
-            __builtin_amdgcn_s_setprio(0);
-        }
-        if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
-        if (tid == kTkTid) {
-            s_tk[slot] = tk;
-            lds_release(&s_tkdone, it + 1u);
-        }
-        uint32_t Tr = kNone;
-        if (Tq < ntiles) {
-            wait_ge(p, &s_tkdone, it + 1u);
-            Tr = uni(s_tk[slot]);
-            if (Tr >= ntiles) Tr = kNone;
-        }
-        if (stamping && Tp < ntiles && lane == 0) {
-            stamp[6] = __builtin_amdgcn_s_memtime();
-            uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
-#pragma unroll
-            for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
-        }
-#pragma unroll
-        for (int j = 0; j < kSt; ++j) { cwp[j][0] = cwl[j]; cwp[j][1] = cwh[j]; }
-        Tp = T;
-        T = Tq;
-        Tq = Tr;
-        ++it;
+        for (int j = 0; j < kSt; ++j)
+            lds_cm_word(s_cs, nc, Tn * kTileTok + (uint32_t)j * kSubTok + wave * kWavePos, lane, cw[j], bad);
+        if (bad && lane == 0) flag_error(p.ctl, KARG(sticky), 16u);   // chunks shorter than a wave range
     };
-    for (;;) {
-        if (!(T < ntiles || Tp < ntiles)) break;
-        step(xa, na, ca, xb, nb, cb, sa, sb);
-        if (!(T < ntiles || Tp < ntiles)) break;
-        step(xb, nb, cb, xa, na, ca, sb, sa);
+    uint32_t it = 0;
+    // chain: the tile this wave emitted in the last iteration, whose stores the next vmcnt(0) wait
+    // completes; each wave then counts itself in s_emc, and the last of the 16 adds the tile to
+    // the pass's emitted counter
+    uint32_t Te = kNone;
+    bool sig_pending = false;
+    auto signal = [&]() {
+        const uint32_t e = it - 1u, es = e & (kRing - 1);
+        uint32_t old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(&s_emc[es], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = uni(old);
+        if (old == (uint32_t)kWaves * (e / kRing + 1u) - 1u && Te < ntiles && lane == 0)
+            __hip_atomic_fetch_add(tkp + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sig_pending = false;
+    };
+
+    for (;;) {   // passes: one, or a chain launch's npasses (per-pass state declared here,
+                 // so none of it is carried from one pass into the next)
+        uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca[kSt][2], cb[kSt][2];
+#pragma unroll
+        for (int j = 0; j < kSt; ++j) { na[j] = nb[j] = 0u; ca[j][0] = ca[j][1] = cb[j][0] = cb[j][1] = 0u; }
+        if (T < ntiles) {
+            if constexpr (kFused) load_fused(p, n, T, wave, lane, xa, na);
+            else if constexpr (kChain) load_tok<true>(p, n, T, wave, lane, xa, na, ca);
+            else load_tok(p, n, T, wave, lane, xa, na, ca);
+        }
+        TileStateT<kSt> sa, sb;
+        uint64_t lbs[kLbWin];
+        uint32_t cwp[kSt][2];   // Tp's chunk-map words
+#pragma unroll
+        for (int j = 0; j < kSt; ++j) cwp[j][0] = cwp[j][1] = 0u;
+        auto step = [&](uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2], uint32_t (&xq)[kSt][8],
+                        uint32_t (&nxtq)[kSt], uint32_t (&cwq)[kSt][2], TileStateT<kSt>& sc, const TileStateT<kSt>& sp) {
+            const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
+            uint64_t stamp[7];
+            const bool stamping = kTiming && p.debug != nullptr;
+            if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map words have landed
+            if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
+            if constexpr (kChain) {
+                if (sig_pending) signal();   // (the wait above completed last iteration's stores)
+                if (T < ntiles) chain_map(T, cw);   // here, before Tq's loads are in flight: fewer live registers
+            }
+            uint32_t cwl[kSt], cwh[kSt];
+#pragma unroll
+            for (int j = 0; j < kSt; ++j) {
+                cwl[j] = kFused ? 0u : uni(cw[j][0]);   // fused: from the front end
+                cwh[j] = kFused ? 0u : uni(cw[j][1]);
+            }
+            if (Tq < ntiles) {
+                if constexpr (kFused) load_fused(p, n, Tq, wave, lane, xq, nxtq);
+                else if constexpr (kChain) load_tok<true>(p, n, Tq, wave, lane, xq, nxtq, cwq);
+                else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
+            }
+            uint32_t tk = kNone;
+            if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(tkp, 1u);
+            asm volatile("" ::: "memory");
+
+            bool lbw = wave == 0;
+            if (T < ntiles) {
+                if (wave >= (uint32_t)kPrioP1Wave) __builtin_amdgcn_s_setprio(kPrioP1);
+                uint32_t m[kSt], live = 0;
+                uint32_t rem2[kSt], C2[kSt];
+                bool nok[kSt];
+                if constexpr (kFused) {
+#pragma unroll
+                    for (int j = 0; j < kSt; ++j)
+                        fused_front<kHash>(p, tab, x[j], nxt[j], (uint64_t)T * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos,
+                                           n, lane, wave, s_stage, rem2[j], nok[j], cwl[j], cwh[j], C2[j]);
+#pragma unroll
+                    for (int j = 0; j < kSt; ++j)
+                        m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem2[j], cwl[j], lane, j, sc, live, nok[j]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kSt; ++j)
+                        m[j] = phase1_tok<kHash>(p, tab, x[j], nxt[j], rem_of(T, j), cwl[j], lane, j, sc, live);
+                }
+                const uint32_t wl = __ballot(live) != 0 ? 1u : 0u;
+                lane_wave_fns<kSt>(m, wave, lane, sc, s_wfn[slot], wl);
+                if constexpr (kFused) {
+                    // a fused range knows its carry-in (C2, from the halo): its wave function is the
+                    // constant one, with the count under C2 and the carry into the next range (the
+                    // range's tokens fill only its first rem2 positions, so the lane functions' own
+                    // carry-out, past the unused positions, is not it)
+#pragma unroll
+                    for (int j = 0; j < kSt; ++j) {
+                        uint32_t L2, M2, off2;
+                        lands1(m[j], sc.mv[j] >> 16, sc.ex[j], C2[j], L2, M2, off2);
+                        const uint32_t cnt = uni(lane_u32(off2 + __popc(L2), 63));
+                        uint32_t co = 1u;
+                        if (nok[j]) {
+                            const uint32_t last = (rem2[j] > kWavePos ? kWavePos : rem2[j]) - 1u;
+                            const uint32_t mb = uni(__builtin_amdgcn_readlane((int)M2, (int)(last >> 4)));
+                            co = ((mb >> (last & 15u)) & 1u) ? 0u : 1u;
+                        }
+                        if (lane == 63) {
+                            const uint32_t g = (uint32_t)j * kWaves + wave;
+                            s_wfn[slot][g][0] = wl << 1;
+                            s_wfn[slot][g][1] = co;
+                            s_wfn[slot][g][2] = cnt;
+                            s_wfn[slot][g][3] = cnt;
+                        }
+                    }
+                }
+                __builtin_amdgcn_s_setprio(0);
+                uint32_t old = 0;
+                if (lane == 0)
+                    old = __hip_atomic_fetch_add(&s_p1cnt[slot], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = uni(old);
+                lbw = old == (uint32_t)kWaves * (it / kRing);
+                if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
+                    resolve_tile<kGroupsTok, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                    if (kChain && lane == 0) st_publish((sw() ? KARG(status) : KARG(status2)) + T, 0ull);   // the next pass's word of T
+                    if (lane == 0) lds_release(&s_rdone, it + 1u);
+                }
+            }
+            if (stamping) stamp[2] = __builtin_amdgcn_s_memtime();
+
+            if (lbw && Tp < ntiles) {
+                uint32_t C = 1u, how = 0xFFFFu, spins = 0, live = 0;
+                uint64_t O = 0ull;
+                const bool lb = Tp > 0;
+                if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+                wait_ge(p, &s_rdone, it);
+                const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
+                const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
+                if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live);
+                live |= (tfl >> 1) & 1u;   // tiles up to and including Tp
+                if (lane == 0) {
+                    const uint64_t end = O + (C == 1u ? tf3 : tf2);
+                    if (C > 1u || O > (uint64_t)Tp * kTileTok || end > n) {
+                        if (C <= 1u) record_error(p, 4u, Tp, 0xFFu, O, end, C);
+                        O = 0; C = 2u;
+                    }
+                    s_C[pslot] = C;
+                    s_O[pslot] = O;
+                    lds_release(&s_lbdone, it + 1u);
+                    const uint64_t fin = C > 1u ? 0ull : O + (C ? tf3 : tf2);
+                    if (Tp > 0) st_publish(p.status + Tp, st_incl(C == 1u ? tf1 : tf0, fin) | (live ? kStLiveIncl : 0ull));
+                    if (2ull * fin > p.out_cap) record_error(p, 2u, Tp, 0xFFu, O, fin, C);
+                    if (Tp == ntiles - 1) {
+                        // The fixpoint: this pass merged nothing, or none of its merges made a key
+                        // component, so the next pass merges nothing (a pair of two tokens this pass
+                        // left alone was looked up here and rejected; a new token is in no key).
+                        const bool fixed = p.done && C <= 1u && (fin == n || !live);
+                        if constexpr (kChain) {   // sc1: the next pass of this launch reads them
+                            __hip_atomic_store(const_cast<uint64_t*>(sw() ? KARG(n_dev) : KARG(total)), fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            __hip_atomic_store(const_cast<uint64_t*>(sw() ? KARG(cstart) : KARG(chunk_off)) + KARG(nchunks), fin, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                            if (fixed) __hip_atomic_store(p.done, KARG(pass_id) + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else {
+                            *KARG(total) = fin;
+                            if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
+                            if (fixed) *p.done = p.pass_id;
+                        }
+                    }
+                    if (kDebugRecord && p.debug) {
+                        uint64_t* d = p.debug + 4ull * Tp;
+                        d[0] = O;
+                        d[1] = ((uint64_t)C << 32) | how;
+                        d[2] = ((uint64_t)tf3 << 32) | tf2;
+                        d[3] = ((uint64_t)tf1 << 32) | tf0;
+                    }
+                }
+            }
+
+            if (stamping) stamp[3] = __builtin_amdgcn_s_memtime();
+            if (Tp < ntiles) {
+                wait_ge(p, &s_lbdone, it + 1u);
+                if (stamping) stamp[4] = __builtin_amdgcn_s_memtime();
+                if (wave >= (uint32_t)kPrioEmWave) __builtin_amdgcn_s_setprio(kPrioEm);
+                const uint32_t Cp = uni(s_C[pslot]);
+                if (Cp <= 1u) {
+                    const uint64_t Op = uni64(s_O[pslot]);
+#pragma unroll
+                    for (int j = 0; j < kSt; ++j) {
+                        const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
+                        emit_tok<kChain>(p, wtok, kFused ? 0u : rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
+                                         s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff, !kFused,
+                                         kChain ? const_cast<uint64_t*>(sw() ? KARG(cstart) : KARG(chunk_off)) : nullptr);
+                    }
+                }
+                __builtin_amdgcn_s_setprio(0);
+            }
+            if (stamping) stamp[5] = __builtin_amdgcn_s_memtime();
+            if (tid == kTkTid) {
+                s_tk[slot] = tk;
+                lds_release(&s_tkdone, it + 1u);
+            }
+            uint32_t Tr = kNone;
+            if (Tq < ntiles) {
+                wait_ge(p, &s_tkdone, it + 1u);
+                Tr = uni(s_tk[slot]);
+                if (Tr >= ntiles) Tr = kNone;
+            }
+            if (stamping && Tp < ntiles && lane == 0) {
+                stamp[6] = __builtin_amdgcn_s_memtime();
+                uint64_t* w = p.debug + 8ull * ntiles + 8ull * ((uint64_t)Tp * kWaves + wave);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
+            }
+#pragma unroll
+            for (int j = 0; j < kSt; ++j) { cwp[j][0] = cwl[j]; cwp[j][1] = cwh[j]; }
+            if constexpr (kChain) {
+                Te = Tp;   // emitted (or failed) in this iteration: counted once its stores complete
+                sig_pending = true;
+            }
+            Tp = T;
+            T = Tq;
+            Tq = Tr;
+            ++it;
+        };
+        for (;;) {
+            if (!(T < ntiles || Tp < ntiles)) break;
+            step(xa, na, ca, xb, nb, cb, sa, sb);
+            if (!(T < ntiles || Tp < ntiles)) break;
+            step(xb, nb, cb, xa, na, ca, sb, sa);
+        }
+        if constexpr (!kChain) {
+            break;
+        } else {
+            // the pass's last stores of this wave, counted; then every tile of the pass emitted
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+            if (sig_pending) signal();
+            if (tid == 0) {
+                SpinClock clk;
+                while (__hip_atomic_load(tkp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
+                    if (clk.expired()) {
+                        flag_error(p.ctl, KARG(sticky), 8u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            __syncthreads();
+            if (pi + 1u >= KARG(npasses)) break;
+            // the next pass: its input count and offsets are this pass's outputs (the arrays
+            // alternate as between separate launches), its status words the other area
+            ++pi;
+            p.status = sw() ? KARG(status2) : KARG(status);
+            tkp = tkp_of();
+            const bool dn = __hip_atomic_load(p.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+            n = uni64(__hip_atomic_load(const_cast<uint64_t*>(sw() ? KARG(total) : KARG(n_dev)), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT));
+            ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
+            if (dn || blockIdx.x >= ntiles) break;   // uniform over the grid / per workgroup
+            if (tid == 0) {
+                s_tk0[0] = atomicAdd(tkp, 1u);
+                s_tk0[1] = atomicAdd(tkp, 1u);
+            }
+            load_starts();
+            __syncthreads();
+            T = uni(s_tk0[0]);
+            Tq = uni(s_tk0[1]);
+            Tp = kNone;
+            Te = kNone;
+            if (T >= ntiles || Tq >= ntiles) Tq = kNone;
+            __syncthreads();
+        }
     }
 }
 
@@ -3102,6 +3302,27 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
     if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2>), g, b, smem, s, p);
     else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1>), g, b, smem, s, p);
     else hipLaunchKernelGGL((seg::scan_tokens_kernel<0>), g, b, 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_chain(const PassParams& p, int device, hipStream_t s) {
+    if (p.n == 0) return hipSuccess;
+    if (!p.status2 || !p.pass_ctr || p.npasses == 0 || p.npasses > kChainMaxPasses || p.nchunks > kChainMaxChunks)
+        return hipErrorInvalidValue;
+    const uint64_t ranges = (p.n + kTokRange - 1) / kTokRange;
+    hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
+    const bool lds = p.hbytes <= kHashLdsMax;
+    const int mode = lds ? (p.hone ? 2 : 1) : 0;
+    const void* fn = mode == 2 ? (const void*)seg::scan_tokens_kernel<2, false, true>
+                     : mode == 1 ? (const void*)seg::scan_tokens_kernel<1, false, true>
+                                 : (const void*)seg::scan_tokens_kernel<0, false, true>;
+    const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
+    const int grid = grid_for(ntiles, device, fn, seg::kThreads, 11 + mode);
+    const size_t smem = lds ? ((size_t)p.hbytes + 1023) & ~(size_t)1023 : 0;
+    const dim3 g((unsigned)grid), b(seg::kThreads);
+    if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2, false, true>), g, b, smem, s, p);
+    else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1, false, true>), g, b, smem, s, p);
+    else hipLaunchKernelGGL((seg::scan_tokens_kernel<0, false, true>), g, b, 0, s, p);
     return hipGetLastError();
 }
 

@@ -1042,3 +1042,84 @@ def test_finish_kernel_fixpoint(case):
                 s.check_workspace(ws.data_ptr(), stream)
     finally:
         _finish(prev)
+
+
+def _chain(on):
+    return blt_amd._lib.lib().blt_debug_set_chain(1 if on else 0)
+
+
+@pytest.mark.parametrize("case", ["doubling", "selfval_text", "chained_text", "many_chunks", "wide_map", "random_map"])
+def test_chain_launch_passes(case):
+    """Round 4: u16 passes of a general map in one persistent launch (launch_scan_chain: the passes
+    meet at a per-pass counter of emitted tiles, the table stays in LDS, each pass's chunk map comes
+    from the chunk starts in LDS).  Against the oracle and against separate launches per pass, with
+    and without the finish kernels, through the host path and the device API (sync and async, chunk
+    offsets): a bounded doubling chain (one launch of 4 or 9 passes), a cyclic map (host-checked
+    batches of up to 4 passes), a chained text map, more chunks than the launch takes (separate
+    launches), a table read from L2, and a random multi-level map."""
+    import torch
+    rng = np.random.default_rng(abs(hash(case)) % (1 << 31))
+    if case == "doubling":         # 1 MiB chunks of 'a': u16 passes 2..5 in one launch, then the finish
+        m, cs = synth.doubling_chain(16), 1 << 20
+        data = np.full((4 << 20) + 77, 97, np.uint8)
+        data[rng.choice(data.size, 40, replace=False)] = 98
+    elif case == "selfval_text":
+        m, cs = synth.SELF_VALUED_MAP, 1 << 20
+        data = synth.text((3 << 20) + 5, seed=17)
+    elif case == "chained_text":
+        m, cs = CHAINED_TEXT_MAP, 65536
+        data = synth.text((2 << 20) + 1234, seed=18)
+    elif case == "many_chunks":    # 1281 chunks: more than a chain launch's chunk starts in LDS
+        m, cs = synth.doubling_chain(12), 4096
+        data = np.full(1280 * 4096 + 100, 97, np.uint8)
+    elif case == "wide_map":       # > 48 KiB of buckets: the table read from L2
+        m = {(int(a), int(b)): 256 + i for i, (a, b) in enumerate(rng.integers(97, 105, (60, 2)))}
+        m.update({(256 + i, 256 + j): 400 + 64 * i + j for i in range(60) for j in range(60)})
+        m.update({(int(a), int(b)): 5000 + i for i, (a, b) in enumerate(rng.integers(0, 256, (6000, 2)))
+                  if (int(a), int(b)) not in m})
+        cs = 1 << 18
+        data = rng.integers(97, 105, (2 << 20) + 3, dtype=np.uint8)
+    else:                          # random multi-level map over a small alphabet
+        keys = [(int(a), int(b)) for a, b in rng.integers(97, 101, (12, 2))]
+        m = {}
+        for i, k in enumerate(keys):
+            m.setdefault(k, 256 + i)
+        vals = sorted(set(m.values()))
+        for i in range(40):
+            a, b = (int(x) for x in rng.choice(vals, 2))
+            if (a, b) not in m:
+                m[(a, b)] = 300 + i
+                vals.append(300 + i)
+        cs = 1 << 17
+        data = rng.integers(97, 101, (1 << 21) + 9, dtype=np.uint8)
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    n = data.size
+    nch = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    prev_c, prev_f = _chain(True), _finish(True)
+    try:
+        for chain_on, fin_on in ((True, True), (True, False), (False, True)):
+            _chain(chain_on)
+            _finish(fin_on)
+            got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+            assert np.array_equal(got, exp), (case, chain_on, fin_on)
+            assert np.array_equal(lens, elens), (case, chain_on, fin_on)
+            for sync in (True, False):
+                d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+                d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+                wsb = s.workspace_size(n, cs)
+                ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+                s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream,
+                                d_off.data_ptr(), sync=sync)
+                torch.cuda.synchronize()
+                offs = d_off.cpu().numpy()
+                assert int(offs[-1]) * 2 == exp.size, (case, chain_on, fin_on, sync)
+                assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), (case, chain_on, fin_on, sync)
+                assert np.array_equal(np.diff(offs) * 2, elens), (case, chain_on, fin_on, sync)
+                s.check_workspace(ws.data_ptr(), stream)
+    finally:
+        _chain(prev_c)
+        _finish(prev_f)

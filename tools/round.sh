@@ -71,10 +71,11 @@ for st in "$@"; do
       find "$O/prof_$a" -name '*kernel_stats.csv' -exec head -4 {} \; | cut -c1-160 ;;
     proff2)
       rows=${a:-multi,wrap,selfval,chain}
+      pd=prof_f2${a:+_${a//,/_}}
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$O/prof_f2" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --only-configs "$rows" \
-        > "$O/prof_f2.log" 2>&1)
-      find "$O/prof_f2" -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-160 ;;
+        -d "$O/$pd" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --only-configs "$rows" \
+        > "$O/$pd.log" 2>&1)
+      find "$O/$pd" -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-160 ;;
     pmc)
       timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --groups "${b:-fetch,write,insts}" -- \
         --workload "$a" --steps 5 --warmup 2 --no-cpu-baseline --no-extra > "$O/pmc_$a.log" 2>&1
