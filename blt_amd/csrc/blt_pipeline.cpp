@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -305,25 +306,33 @@ bool env_on(const char* name, bool dflt) {
 void map_output(int fd, size_t total, size_t est, OutMap* om) {
     if (ftruncate(fd, (off_t)total) != 0) return;
     om->sized = true;
-    preallocate(fd, std::min(est, total));
     void* m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     if (m == MAP_FAILED) return;
     om->m = static_cast<uint8_t*>(m);
     om->total = total;
-    if (env_on("BLT_OUT_POPULATE", true)) {   // (env: A/B runs)
-        // 2 MiB-aligned pieces over 4 threads; best effort (older kernels: EINVAL, the copies fault)
+    const size_t len = std::min(est, total);
+    // (env: A/B runs) 0 no prefault, 1 fallocate then populate, 2 populate only (it allocates
+    // too), with MADV_HUGEPAGE first when BLT_OUT_HUGE is set (tmpfs huge pages where the host
+    // allows them: 512x fewer faults)
+    const char* pv = getenv("BLT_OUT_POPULATE");
+    const int mode = (pv && *pv) ? atoi(pv) : 1;
+    const char* tv = getenv("BLT_OUT_THREADS");
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(16, (tv && *tv) ? (size_t)atoi(tv) : 4));
+    if (env_on("BLT_OUT_HUGE", false)) (void)madvise(m, total, MADV_HUGEPAGE);
+    if (mode == 1 || mode == 0) preallocate(fd, len);
+    if (mode >= 1) {
+        // 2 MiB-aligned pieces over nt threads; best effort (older kernels: EINVAL, the copies fault)
         constexpr size_t kPiece = size_t(2) << 20;
-        const size_t len = std::min(est, total);
         const size_t pieces = (len + kPiece - 1) / kPiece;
-        auto part = [&](size_t t, size_t nt) {
+        auto part = [&](size_t t) {
             for (size_t i = t; i < pieces; i += nt) {
                 const size_t off = i * kPiece;
                 if (madvise(om->m + off, std::min(kPiece, len - off), MADV_POPULATE_WRITE) != 0) return;
             }
         };
-        std::thread th[3];
-        for (size_t t = 0; t < 3; ++t) th[t] = std::thread(part, t + 1, size_t(4));
-        part(0, 4);
+        std::vector<std::thread> th;
+        for (size_t t = 1; t < nt; ++t) th.emplace_back(part, t);
+        part(0);
         for (auto& t : th) t.join();
     }
     // (env experiment) the whole mapping page-locked for the runtime's copies

@@ -8,7 +8,10 @@ namespace blt {
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
 constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
-constexpr uint64_t kTilePosTok = 32768;        // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
+#ifndef BLT_TILE_TOK
+#define BLT_TILE_TOK 32768
+#endif
+constexpr uint64_t kTilePosTok = BLT_TILE_TOK;  // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
 constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chunk-map word each)
 #ifndef BLT_TILE_BYTES
 #define BLT_TILE_BYTES 32768

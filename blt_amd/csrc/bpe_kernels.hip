@@ -226,10 +226,12 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 // A launch told its workspace is zeroed (p.ws_check) whose tiles reach past the status words known
 // zero refuses: error bit 32 (one workgroup flags it) and no output; its workgroups claim no tile
 // but still count themselves out, so the self-reset zeroes its ntiles words as usual.  The word is
-// read at the workgroup's start (a scalar load, written before the launch on its stream) and tested
-// after the table copy, off the critical path.
+// read at the workgroup's start (written before the launch on its stream) and tested after the
+// table copy, off the critical path.  A relaxed atomic load, not a volatile one: measured, the
+// volatile load (which the backend orders with waits) made the headline byte pass 6 % slower
+// (cfg3 0.556 -> 0.590 ms, the check compiled out 0.554; BLT_COVER_LOAD switches for A/B).
 #ifndef BLT_COVER_LOAD
-#define BLT_COVER_LOAD 0
+#define BLT_COVER_LOAD 1
 #endif
 __device__ __forceinline__ uint32_t ws_cover(const PassParams& p) {
 #ifdef BLT_WS_NOCHECK   // (experiment: no coverage check)
@@ -244,6 +246,15 @@ __device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles,
     if (ntiles <= cover) return false;
     if (blockIdx.x == 0 && threadIdx.x == 0) flag_error(p.ctl, KARG(sticky), 32u);
     return true;
+}
+
+// 16 x the lane index, computed where it is used: inline asm is never hoisted, so a rare branch
+// (a chunk or buffer end in a wave range) does not keep a per-lane constant live across the
+// byte pass's loop (the register allocator spilled two such VGPRs to scratch).
+__device__ __forceinline__ uint32_t lane16_here() {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 4, %0" : "=v"(l));
+    return l;
 }
 
 // Lane i's 64-bit value from its two halves.  readlane returns int: cast each half to uint32_t
@@ -1095,12 +1106,13 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         const uint32_t rem = ti.rn > wrel ? ti.rn - wrel : 0u;
         const bool has_end = bnext - 1u - wrel < kWavePos;
         if (rem <= kWavePos || has_end) {
-            const int32_t r = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
+            const uint32_t l16 = lane16_here();
+            const int32_t r = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - (int32_t)l16;
             const uint32_t vmask = r >= 16 ? 0xFFFFu : (r <= 0 ? 0u : ((1u << r) - 1u));
             uint32_t mm = m[j] & ((vmask >> 1) | (r > 16 ? 0x8000u : 0u));
             uint32_t forced = (r >= 1 && r <= 16) ? (1u << (r - 1)) : 0u;   // the buffer's last position
             if (has_end) {                                                   // chunk end b - 1 here
-                const uint32_t e = bnext - 1u - wrel - 16u * (uint32_t)lane;
+                const uint32_t e = bnext - 1u - wrel - l16;
                 if (e < 16u) { mm &= ~(1u << e); forced |= 1u << e; }
             }
             if (__ballot(forced != 0)) {   // a cut merge emits its raw byte
@@ -1594,7 +1606,7 @@ __device__ __forceinline__ void emit_tile(const PassParams& p, uint32_t Tp, cons
         const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
         const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
         if (cstart) {
-            const uint32_t e = cnext - wrel - 16u * (uint32_t)lane;
+            const uint32_t e = cnext - wrel - lane16_here();
             if (e < 16u) KARG(chunk_off)[kc] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
         }
         sr[j].L = L;

@@ -18,6 +18,7 @@
 #   pmc:WL[:GROUPS]    tools/pmc_profile.py on bench.py --workload WL (groups default fetch,write,insts)
 #   pmcf2:ROW[:GROUPS] PMC of one f2 row (tools/f2_row.py: every kernel of its calls, traffic per call)
 #   cli[:ENV]          tools/cli_phases.py: the CLI's BLT_CLI_TIMING phases on 1 GiB, the HIP start-up probe
+#   copyprobe          tools/copy_probe.cpp: host<->device copy rates by kind of host memory
 #   py:SCRIPT[:ARGS]   a tool script under its own time limit
 #   resources          -Rpass-analysis=kernel-resource-usage of the kernel source (CPU only)
 set -e
@@ -88,9 +89,15 @@ for st in "$@"; do
     cli)
       # BLT_CLI_TIMING phases of the CLI on 1 GiB (tools/cli_phases.py), cli:ENV (NAME=VALUE, commas)
       [ -x build/hip_init_probe ] || /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/hip_init_probe.cpp -o build/hip_init_probe
+      echo "shmem THP: $(cat /sys/kernel/mm/transparent_hugepage/shmem_enabled 2>/dev/null)" 
       nb=$((nb + 1))
       timeout -k 10 300 python tools/cli_phases.py --out "$O/cli_phases_$nb.json" ${a:+--env "$a"} > "$O/cli_$nb.log" 2>&1
       python -c "import json;d=json.load(open('$O/cli_phases_$nb.json'));print(d.get('hip_init_probe'));[print(r['wall_s'],r['GBps']) for r in d['runs']]" ;;
+    copyprobe)
+      # host<->device copy rates from the CLI's kinds of host memory (tools/copy_probe.cpp)
+      [ -x build/copy_probe ] || /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/copy_probe.cpp -o build/copy_probe
+      timeout -k 10 120 build/copy_probe > "$O/copy_probe.txt" 2>&1
+      cat "$O/copy_probe.txt" ;;
     py)
       # any tool script: py:tools/x.py[:ARGS] (ARGS + for spaces), output py_<n>.log
       nb=$((nb + 1))
