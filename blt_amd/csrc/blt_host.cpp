@@ -1700,8 +1700,20 @@ int blt_basic_process_chunk(const uint8_t* in, size_t n, uint8_t* out, size_t ou
 // that call will use, left in the context pool.  Failures are left for the call itself to report.
 void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) try {
     if (!h || !n || !cs) return;
+    // BLT_CLI_TIMING: the setup's steps (seconds from this call's start), on stderr
+    const bool timing = getenv("BLT_CLI_TIMING") != nullptr;
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    auto stamp = [&](const char* what) {
+        if (!timing) return;
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        fprintf(stderr, "blt timing: prewarm step: %s +%.4f s\n", what,
+                (double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec));
+    };
     HostPlan plan;
     if (host_plan(h, n, cs, n_gpus, &plan) != 0) return;
+    stamp("device count (runtime up)");
     const uint64_t g = plan.devs.size();
     const uint64_t nchunks = (n + cs - 1) / cs;
     const uint64_t share = (nchunks + g - 1) / g * cs;
@@ -1714,12 +1726,18 @@ void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) t
         if (hipSetDevice(dev) != hipSuccess) return;
         DevTables* t;
         if (device_tables(h, dev, &t) != 0) return;
+        stamp("device tables");
         DevCtx* c = ctx_acquire(dev);
         if (!c) return;
         CtxGuard guard{c};
+        stamp("context (streams)");
         if (plan.multi) {
             for (int k = 0; k < slots; ++k)
                 if (pipe_slot_ready(h, c->pipe[k], std::min(win, n), cs) != 0) return;
+            stamp("pipeline slots");
+            // the code object's load, off the first window's path
+            if (blt::launch_noop(c->pipe[0].stream) == hipSuccess) (void)hipStreamSynchronize(c->pipe[0].stream);
+            stamp("code object loaded (first launch)");
         } else {
             const WsLayout L = ws_layout(h->single_pass, n, cs);
             uint8_t* offp = reinterpret_cast<uint8_t*>(c->d_off);

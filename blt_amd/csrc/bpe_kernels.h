@@ -125,6 +125,9 @@ hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipS
 // else k_last) gives *tot_final and, when it wrote off1, the caller's chunk offsets.
 hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const uint64_t* off1, uint64_t* chunk_off,
                               uint64_t nchunks, uint32_t k_last, uint64_t* tot_final, hipStream_t s);
+// An empty kernel: the first launch of any kernel loads the library's code object on the device
+// (the CLI's start-up does it on its helper thread, beside the input's mmap).
+hipError_t launch_noop(hipStream_t s);
 // Test hook: runs the kernels' error path once (ctl nullable, sticky the handle's error word).
 hipError_t launch_inject_error(uint32_t* ctl, uint32_t* sticky, hipStream_t s);
 

@@ -230,6 +230,9 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 // table copy, off the critical path.  A relaxed atomic load, not a volatile one: measured, the
 // volatile load (which the backend orders with waits) made the headline byte pass 6 % slower
 // (cfg3 0.556 -> 0.590 ms, the check compiled out 0.554; BLT_COVER_LOAD switches for A/B).
+#ifndef BLT_SHIFT16   // u16 ranges with no merge emitted from registers (emit_shift16); 0 for A/B
+#define BLT_SHIFT16 1
+#endif
 #ifndef BLT_COVER_LOAD
 #define BLT_COVER_LOAD 1
 #endif
@@ -2200,6 +2203,61 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
     return m;
 }
 
+// A u16 wave range none of whose pairs merged (every position lands): its 1024 tokens go out as
+// they are, shifted to the range's output offset, straight from registers.  Lane l holds output
+// bytes [32 l, 32 l + 32) of the range (v[0..7]), at byte rg + 32 l past the 16-byte boundary ab;
+// it stores aligned blocks 2 l (lane l - 1's last rg bytes, then its own first 16 - rg: one DPP
+// fetch of the previous lane's registers) and 2 l + 1 (its own).  Lane 0 stores the head of block 0
+// and lane 63 the partial block 128 token by token, as emit_dense does.  (A general map's late
+// passes, e.g. the self-valued map's, merge a few pairs in 256 MiB: nearly every range used to take
+// the stage round trip, 16 ds_write_b16 per lane, only to copy its tokens one slot to the left.)
+// Aligned blocks 2 l and 2 l + 1 from the 64-byte concatenation w (lane l - 1's bytes, then lane
+// l's) at byte offset 4 D + r (D compile-time: the shift has four cases, one per dword).
+template <int D>
+__device__ __forceinline__ void shift_blocks(const uint32_t (&w)[16], uint32_t r, u32x4& B0, u32x4& B1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        B0[q] = funnel(w[D + q + 1], w[D + q], r);
+        B1[q] = funnel(w[D + q + 5], w[D + q + 4], r);
+    }
+}
+template <int kPol = BLT_STPOL, int kPol16 = 0>
+__device__ __forceinline__ void emit_shift16(const uint32_t (&v)[8], uint32_t rg, __amdgpu_buffer_rsrc_t ro,
+                                             uint32_t ab, int lane) {
+    const uint32_t o = ab + 32u * (uint32_t)lane;
+    if (rg == 0) {   // uniform
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[0], v[1], v[2], v[3]}, ro, (int)o, 0, kPol);
+        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[4], v[5], v[6], v[7]}, ro, (int)(o + 16u), 0, kPol);
+        return;
+    }
+    uint32_t w[16];   // lane l - 1's 32 bytes, then lane l's
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        w[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[q], (int)v[q], 0x138, 0xF, 0xF, false);
+        w[8 + q] = v[q];
+    }
+    // block 2 l = concatenation bytes [32 - rg, 48 - rg), block 2 l + 1 = [48 - rg, 64 - rg)
+    const uint32_t b0 = 32u - rg, d = b0 >> 2, r = b0 & 3u;   // uniform: d in 4..7, r in {0, 2}
+    u32x4 B0, B1;
+    if (d == 4) shift_blocks<4>(w, r, B0, B1);
+    else if (d == 5) shift_blocks<5>(w, r, B0, B1);
+    else if (d == 6) shift_blocks<6>(w, r, B0, B1);
+    else shift_blocks<7>(w, r, B0, B1);
+    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(B0, ro, (int)o, 0, kPol);
+    __builtin_amdgcn_raw_buffer_store_b128(B1, ro, (int)(o + 16u), 0, kPol);
+    if (lane == 0 || lane == 63) {
+        // lane 0: its first (16 - rg) / 2 tokens at ab + rg; lane 63: its last rg / 2 at ab + 2048
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint16_t tok = (uint16_t)(v[k >> 1] >> (16 * (k & 1)));
+            if (lane == 0 && 2u * (uint32_t)k < 16u - rg)
+                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, kPol16);
+            if (lane == 63 && 2u * (uint32_t)k >= 32u - rg)
+                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 2048u + 2u * k - (32u - rg)), 0, kPol16);
+        }
+    }
+}
+
 // Emission of sub-tile j's wave range (as emit_tile), its chunk start from the chunk-map word.
 // rem: tokens from the range start to the buffer end; wtok: the range's first input token.
 // kChain (chain launches): every store sc1 (write-through: the next pass of the same launch reads
@@ -2244,6 +2302,12 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
     if (inplace && wcnt == (rem < kWavePos ? rem : kWavePos) && O + goff == wtok) return;
+#if BLT_SHIFT16
+    if (__ballot(L != 0xFFFFu) == 0) {   // every position lands: the tokens as they are, shifted
+        emit_shift16<kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(st.v[j], gb & 15u, ro, gb & ~15u, lane);
+        return;
+    }
+#endif
     // one part: the stage holds the range's at most 1024 tokens
     const uint32_t x0 = wave * (uint32_t)kStageTok;   // the wave's stage, logical bytes
     stage_b16_pad(st.v[j], L, stg, x0 + (gb & 15u) + 2u * lane_off);
@@ -2857,12 +2921,17 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                                         __HIP_MEMORY_SCOPE_AGENT));
             ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
             if (dn || blockIdx.x >= ntiles) break;   // uniform over the grid / per workgroup
+            // the iteration counters start over: the ring words count arrivals per iteration (phase 1
+            // only where an iteration has a tile), so a pass's drain iterations would skew them
             if (tid == 0) {
                 s_tk0[0] = atomicAdd(tkp, 1u);
                 s_tk0[1] = atomicAdd(tkp, 1u);
+                for (int r = 0; r < kRing; ++r) { s_p1cnt[r] = 0; s_emc[r] = 0; }
+                s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
             }
             load_starts();
             __syncthreads();
+            it = 0;
             T = uni(s_tk0[0]);
             Tq = uni(s_tk0[1]);
             Tp = kNone;
@@ -3383,6 +3452,12 @@ hipError_t launch_finish(const PassParams& p, int device, hipStream_t s) {
     if (mode == 2) hipLaunchKernelGGL((finish_chunks_kernel<2>), g, b, smem, s, p);
     else if (mode == 1) hipLaunchKernelGGL((finish_chunks_kernel<1>), g, b, smem, s, p);
     else hipLaunchKernelGGL((finish_chunks_kernel<0>), g, b, 0, s, p);
+    return hipGetLastError();
+}
+
+__global__ void noop_kernel() {}
+hipError_t launch_noop(hipStream_t s) {
+    hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, s);
     return hipGetLastError();
 }
 
