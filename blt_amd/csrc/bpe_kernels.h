@@ -8,6 +8,8 @@ namespace blt {
 constexpr int kSub = 4;                       // sub-tiles per look-back tile
 constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (kSub * threads * 16)
 constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
+// (16384 measured and rejected: no VGPR spills, but twice the tiles and look-backs; f2 chain
+// 0.672 -> 0.804 ms, selfval 1.39 -> 1.77, multi 0.537 -> 0.575; profiles/r04_shift16_ab.txt)
 #ifndef BLT_TILE_TOK
 #define BLT_TILE_TOK 32768
 #endif

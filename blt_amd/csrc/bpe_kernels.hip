@@ -230,8 +230,16 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 // table copy, off the critical path.  A relaxed atomic load, not a volatile one: measured, the
 // volatile load (which the backend orders with waits) made the headline byte pass 6 % slower
 // (cfg3 0.556 -> 0.590 ms, the check compiled out 0.554; BLT_COVER_LOAD switches for A/B).
-#ifndef BLT_SHIFT16   // u16 ranges with no merge emitted from registers (emit_shift16); 0 for A/B
-#define BLT_SHIFT16 1
+// u16 ranges with no merge emitted from registers (emit_shift16).  Off: measured slower
+// (profiles/r04_shift16_ab.txt): selfval, whose late passes it targets, 1.38 -> 1.54 ms with the
+// first version; with the head/tail stores folded into one loop every f2 row lost, also rows that
+// never take the path (chain 0.669 -> 0.800 ms, multi 0.535 -> 0.72): the extra code costs the
+// scan's registers and schedule more than the stage round trip it replaces.
+#ifndef BLT_SHIFT16
+#define BLT_SHIFT16 0
+#endif
+#ifndef BLT_SHIFT_DPP   // emit_shift16's fetch of the previous lane: DPP wave shift (1) or ds_bpermute (0)
+#define BLT_SHIFT_DPP 1
 #endif
 #ifndef BLT_COVER_LOAD
 #define BLT_COVER_LOAD 1
@@ -255,6 +263,9 @@ __device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles,
 // (a chunk or buffer end in a wave range) does not keep a per-lane constant live across the
 // byte pass's loop (the register allocator spilled two such VGPRs to scratch).
 __device__ __forceinline__ uint32_t lane16_here() {
+#ifdef BLT_NO_LANE16_ASM   // (A/B: the plain expression, which the compiler hoists)
+    return 16u * (threadIdx.x & 63u);
+#endif
     uint32_t l;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 4, %0" : "=v"(l));
     return l;
@@ -2233,7 +2244,11 @@ __device__ __forceinline__ void emit_shift16(const uint32_t (&v)[8], uint32_t rg
     uint32_t w[16];   // lane l - 1's 32 bytes, then lane l's
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
+#if BLT_SHIFT_DPP
         w[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[q], (int)v[q], 0x138, 0xF, 0xF, false);
+#else
+        w[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (lane > 0 ? lane - 1 : 0), (int)v[q]);
+#endif
         w[8 + q] = v[q];
     }
     // block 2 l = concatenation bytes [32 - rg, 48 - rg), block 2 l + 1 = [48 - rg, 64 - rg)
@@ -2245,15 +2260,21 @@ __device__ __forceinline__ void emit_shift16(const uint32_t (&v)[8], uint32_t rg
     else shift_blocks<7>(w, r, B0, B1);
     if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(B0, ro, (int)o, 0, kPol);
     __builtin_amdgcn_raw_buffer_store_b128(B1, ro, (int)(o + 16u), 0, kPol);
+    // lane 0: its first h0 = (16 - rg) / 2 tokens at ab + rg; lane 63: its last h63 = rg / 2 at
+    // ab + 2048; both in the same store instructions (h0 + h63 = 8: at most 7 of them)
+    const uint32_t h0 = (16u - rg) >> 1, h63 = rg >> 1, hm = h0 > h63 ? h0 : h63;
     if (lane == 0 || lane == 63) {
-        // lane 0: its first (16 - rg) / 2 tokens at ab + rg; lane 63: its last rg / 2 at ab + 2048
+        const uint32_t k0 = lane == 0 ? 0u : 16u - h63, hl = lane == 0 ? h0 : h63;
+        const uint32_t a0 = lane == 0 ? ab + rg : ab + 2048u;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint16_t tok = (uint16_t)(v[k >> 1] >> (16 * (k & 1)));
-            if (lane == 0 && 2u * (uint32_t)k < 16u - rg)
-                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, kPol16);
-            if (lane == 63 && 2u * (uint32_t)k >= 32u - rg)
-                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 2048u + 2u * k - (32u - rg)), 0, kPol16);
+        for (uint32_t k = 0; k < 7u; ++k) {
+            if (k >= hm) break;   // uniform
+            const uint32_t kk = k0 + k;
+            uint32_t wv = v[0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) wv = (kk >> 1) == (uint32_t)q ? v[q] : wv;
+            if (k < hl)
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(wv >> (16 * (kk & 1u))), ro, (int)(a0 + 2u * k), 0, kPol16);
         }
     }
 }

@@ -34,8 +34,8 @@ for st in "$@"; do
   echo "== $st $(date +%T)"
   case $kind in
     tests)
-      # tests[:K] runs only the tests whose names match K (pytest -k)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${a:+-k "$a"} \
+      # tests[:K] runs only the tests whose names match K (pytest -k; + for spaces)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${a:+-k "${a//+/ }"} \
         > "$O/tests${a:+_$a}.log" 2>&1 || { tail -40 "$O/tests${a:+_$a}.log"; exit 1; }
       tail -2 "$O/tests${a:+_$a}.log" ;;
     smoke)
