@@ -733,8 +733,12 @@ int run_chain(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint
     return 0;
 }
 
-// Test hook (blt_debug_set_chain): 0 runs every u16 pass as its own launch.
-std::atomic<int> g_chain{1};
+// Chain launches are off by default: measured, one persistent launch of a chain's passes costs
+// what the separate launches do (f2 chain 0.666 ms either way, selfval 1.34 -> 1.39 ms with them;
+// profiles/r04_chain_ab.txt): a pass's barrier drains and refills every workgroup's pipeline as a
+// kernel boundary does, and the launch loses the nt cache policy to the sc1 hand-off.  Test hook
+// blt_debug_set_chain(1), or BLT_CHAIN=1 in the environment, turns them on.
+std::atomic<int> g_chain{getenv("BLT_CHAIN") && getenv("BLT_CHAIN")[0] == '1' ? 1 : 0};
 
 // Passes 1 and 2 of a general map in one launch (blt::launch_scan_fused): bytes d_in to the second
 // pass's tokens in d_out, its total, chunk offsets and done word as u16 pass 1's.

@@ -1172,7 +1172,7 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 // ---- tile resolve (one wave): group carries and offsets, tile function, publish -------------
 // kLive (u16 scan kernel): the groups' live bits (wfn[g][0] bit 1) are ORed into the tile's
 // status word and into tfn[0] bit 1.
-template <int NG = kGroups, bool kLive = false>
+template <int NG = kGroups, bool kLive = false, bool kFresh = false>
 __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane, const uint32_t (*wfn)[4],
                                              uint32_t (*gin)[4], uint32_t* tfn) {
     uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
@@ -1181,7 +1181,7 @@ __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, in
     if (kLive) gi &= 1u;
     const uint64_t nonid = __ballot(!gi);
     const uint64_t cmask = __ballot(gco);
-    const uint64_t below = nonid & ((1ull << lane) - 1ull);
+    const uint64_t below = nonid & ((1ull << (kFresh ? lane16_here() >> 4 : (uint32_t)lane)) - 1ull);   // (kFresh: lb_issue)
     const uint32_t hb = below != 0;
     const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
     const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
@@ -1220,11 +1220,25 @@ __device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, in
 // ---- look-back (wave 0) ------------------------------------------------------------------
 // Lane l of window q reads the status of tile k - l - 64 q; tiles before 0 read as an
 // inclusive prefix with carry 1 at offset 0.
+// kFresh (the u16 scan kernel): 32-bit tile indices and the lane index computed here.  Hoisted out
+// of its loop as 64-bit per-lane constants they were spilled to scratch, and every look-back
+// waited for the reload's vmcnt, i.e. for the next tile's loads too (measured: f2 rows 1.5-3 %
+// faster without; the byte pass, which does not spill them, 1 % slower with it).
+template <bool kFresh = false>
 __device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lane, uint64_t (&s)[kLbWin]) {
+    if constexpr (kFresh) {
+        const int32_t l = (int32_t)(lane16_here() >> 4);
 #pragma unroll
-    for (int q = 0; q < kLbWin; ++q) {
-        const int64_t idx = k - lane - 64 * q;
-        s[q] = idx >= 0 ? st_read(p.status + idx) : st_incl(1u, 0ull);
+        for (int q = 0; q < kLbWin; ++q) {
+            const int32_t idx = (int32_t)k - l - 64 * q;
+            s[q] = idx >= 0 ? st_read(p.status + (uint32_t)idx) : st_incl(1u, 0ull);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kLbWin; ++q) {
+            const int64_t idx = k - lane - 64 * q;
+            s[q] = idx >= 0 ? st_read(p.status + idx) : st_incl(1u, 0ull);
+        }
     }
 }
 
@@ -1295,6 +1309,7 @@ struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never 
 // Call it from wave-uniform control flow only (a branch on an SGPR value): its DPP scans
 // (row_bcast) need the whole wave, and measured in a kernel that reached it through a branch on a
 // VGPR value (finish_chunks_kernel's first version), the window sums came out wrong.
+template <bool kFresh = false>
 __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (&s)[kLbWin], uint32_t& C,
                           uint64_t& O, uint32_t& how, uint32_t& spins, uint32_t& live, uint32_t* bad_out = nullptr) {
     TileFn acc = {0u, 1u, 0ull, 0ull};   // tiles between the windows read and Tp (identity)
@@ -1336,7 +1351,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 return;
             }
             __builtin_amdgcn_s_sleep(1);
-            lb_issue(p, k, lane, s);
+            lb_issue<kFresh>(p, k, lane, s);
             continue;
         }
         if (qs < 0) {   // no inclusive prefix in 256 tiles: fold them into acc, read further back
@@ -1354,7 +1369,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
             acc = w;
             k -= 64 * kLbWin;
             ++rounds;
-            lb_issue(p, k, lane, s);
+            lb_issue<kFresh>(p, k, lane, s);
             continue;
         }
         uint32_t c = 0;
@@ -1857,7 +1872,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             old = uni(old);
             lbw = old == (uint32_t)kWaves * (it / kRing);
             if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                resolve_tile<kGroups, kLive>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                resolve_tile<kGroups, kLive, kMode != 0>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                 if (lane == 0) lds_release(&s_rdone, it + 1u);
                 if (stamping && lane == 0) p.debug[4ull * ntiles + 4ull * T] = __builtin_amdgcn_s_memrealtime();
             }
@@ -1870,13 +1885,13 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
             uint32_t C = 1u, how = 0xFFFFu, spins = 0, bad = 0, live = 0;
             uint64_t O = 0ull;
             const bool lb = Tp > 0;
-            if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+            if (lb) lb_issue<kMode != 0>(p, (int64_t)Tp - 1, lane, lbs);
             const uint64_t rt_snap = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
             // Tp was resolved last iteration: its tile function is read while the snapshot flies
             wait_ge(p, &s_rdone, it);
             const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
             const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-            if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live, kTiming ? &bad : nullptr);
+            if (lb) lb_finish<kMode != 0>(p, Tp, lane, lbs, C, O, how, spins, live, kTiming ? &bad : nullptr);
             live |= (tfl >> 1) & 1u;   // tiles up to and including Tp (kLive; 0 otherwise)
             if (lane == 0) {
                 const uint64_t end = O + (C == 1u ? tf3 : tf2);
@@ -2315,7 +2330,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t M = (mc & ~rodd & 0x5555u) | (rodd & 0xAAAAu);
     const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
     if (cstart) {
-        const uint32_t e = (cwl & 0x7FFu) - 16u * (uint32_t)lane;
+        const uint32_t e = (cwl & 0x7FFu) - lane16_here();
         if (e < 16u)
             coff_store((kChain ? coff_chain : KARG(chunk_off)) + cwh, O + goff + lane_off + __popc(L & ((1u << e) - 1u)),
                        kChain);
@@ -2807,7 +2822,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 old = uni(old);
                 lbw = old == (uint32_t)kWaves * (it / kRing);
                 if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
-                    resolve_tile<kGroupsTok, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
+                    resolve_tile<kGroupsTok, true, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
                     if (kChain && lane == 0) st_publish((sw() ? KARG(status) : KARG(status2)) + T, 0ull);   // the next pass's word of T
                     if (lane == 0) lds_release(&s_rdone, it + 1u);
                 }
@@ -2818,11 +2833,11 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 uint32_t C = 1u, how = 0xFFFFu, spins = 0, live = 0;
                 uint64_t O = 0ull;
                 const bool lb = Tp > 0;
-                if (lb) lb_issue(p, (int64_t)Tp - 1, lane, lbs);
+                if (lb) lb_issue<true>(p, (int64_t)Tp - 1, lane, lbs);
                 wait_ge(p, &s_rdone, it);
                 const uint32_t tfl = uni(s_tfn[pslot][0]), tf1 = uni(s_tfn[pslot][1]);
                 const uint32_t tf0 = tfl & 1u, tf2 = uni(s_tfn[pslot][2]), tf3 = uni(s_tfn[pslot][3]);
-                if (lb) lb_finish(p, Tp, lane, lbs, C, O, how, spins, live);
+                if (lb) lb_finish<true>(p, Tp, lane, lbs, C, O, how, spins, live);
                 live |= (tfl >> 1) & 1u;   // tiles up to and including Tp
                 if (lane == 0) {
                     const uint64_t end = O + (C == 1u ? tf3 : tf2);
