@@ -16,6 +16,7 @@
 #   prof:WL            rocprofv3 --kernel-trace --stats of bench.py --workload WL (cfg2|cfg3|cfg5)
 #   proff2[:ROWS]      rocprofv3 kernel stats of the f2 rows (bench.py --only-configs ROWS)
 #   pmc:WL[:GROUPS]    tools/pmc_profile.py on bench.py --workload WL (groups default fetch,write,insts)
+#   pmc4:G             PMC traffic of cfg4's per-rank shard of G GiB (N = 8/4/2: G = 1/2/4)
 #   pmcf2:ROW[:GROUPS] PMC of one f2 row (tools/f2_row.py: every kernel of its calls, traffic per call)
 #   cli[:ENV]          tools/cli_phases.py: the CLI's BLT_CLI_TIMING phases on 1 GiB, the HIP start-up probe
 #   copyprobe          tools/copy_probe.cpp: host<->device copy rates by kind of host memory
@@ -71,9 +72,10 @@ for st in "$@"; do
         --workload "$a" > "$O/prof_$a.log" 2>&1)
       find "$O/prof_$a" -name '*kernel_stats.csv' -exec head -4 {} \; | cut -c1-160 ;;
     proff2)
+      # proff2[:ROWS[:ENV]]  (ENV: NAME=VALUE for the profiled run, e.g. BLT_CHAIN=0)
       rows=${a:-multi,wrap,selfval,chain}
-      pd=prof_f2${a:+_${a//,/_}}
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+      pd=prof_f2${a:+_${a//,/_}}${b:+_${b//=/}}
+      (cd /tmp && export TMPDIR=/tmp && { [ -z "$b" ] || export "$b"; } && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$O/$pd" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --only-configs "$rows" \
         > "$O/$pd.log" 2>&1)
       find "$O/$pd" -name '*kernel_stats.csv' -exec head -12 {} \; | cut -c1-160 ;;
@@ -81,6 +83,11 @@ for st in "$@"; do
       timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --groups "${b:-fetch,write,insts}" -- \
         --workload "$a" --steps 5 --warmup 2 --no-cpu-baseline --no-extra > "$O/pmc_$a.log" 2>&1
       tail -3 "$O/pmc_$a.log" ;;
+    pmc4)
+      # cfg4's per-rank shard of G GiB (the N = 8/4/2 shard sizes 1/2/4 GiB): pmc4:G
+      timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_cfg4_$a" --groups fetch,write -- \
+        --workload cfg4 --total-bytes $((a << 30)) --steps 3 --warmup 1 --no-cpu-baseline --no-extra > "$O/pmc_cfg4_$a.log" 2>&1
+      tail -2 "$O/pmc_cfg4_$a.log" ;;
     pmcf2)
       # 5 asynchronous calls (tools/f2_row.py): traffic per call = totals / 5
       timeout -k 10 900 python tools/pmc_profile.py "$O/pmc_$a" --kernel "" --script tools/f2_row.py --calls 5 \
