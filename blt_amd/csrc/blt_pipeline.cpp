@@ -311,11 +311,15 @@ void map_output(int fd, size_t total, size_t est, OutMap* om) {
     om->m = static_cast<uint8_t*>(m);
     om->total = total;
     const size_t len = std::min(est, total);
-    // (env: A/B runs) 0 no prefault, 1 fallocate then populate, 2 populate only (it allocates
-    // too), with MADV_HUGEPAGE first when BLT_OUT_HUGE is set (tmpfs huge pages where the host
-    // allows them: 512x fewer faults)
+    // (env: A/B runs) 0 fallocate only (the default), 1 fallocate then populate (MADV_POPULATE_WRITE,
+    // BLT_OUT_THREADS threads), 2 populate only (it allocates too), with MADV_HUGEPAGE first when
+    // BLT_OUT_HUGE is set (tmpfs huge pages where the host allows them; the GPU box's shmem THP is
+    // "never").  Measured (profiles/r04_cli_phases.json): populating makes the device-to-host copies
+    // 3x faster (tools/copy_probe.cpp: 0.139 -> 0.042 s per GiB), but the page-fault storm holds the
+    // process's mmap lock while the HIP runtime starts on the other thread, and its start-up went
+    // from 0.11-0.13 to 0.23 s: no net gain, so the writes fault their own pages.
     const char* pv = getenv("BLT_OUT_POPULATE");
-    const int mode = (pv && *pv) ? atoi(pv) : 1;
+    const int mode = (pv && *pv) ? atoi(pv) : 0;
     const char* tv = getenv("BLT_OUT_THREADS");
     const size_t nt = std::max<size_t>(1, std::min<size_t>(16, (tv && *tv) ? (size_t)atoi(tv) : 4));
     if (env_on("BLT_OUT_HUGE", false)) (void)madvise(m, total, MADV_HUGEPAGE);
