@@ -578,7 +578,19 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 struct WsLayout {
     uint64_t ntiles, nchunks;
     uint64_t ctl, status, total, off_a, off_b, cmap, gstat, stat2, pctr, bytes, zero_bytes;
+    // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
+    // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
+    uint64_t sp_holes, sp_cs, sp_bits0, sp_bits1, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr;
+    uint32_t sp_cap;
 };
+// Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
+constexpr uint32_t kMaxBoundedPasses = 64;
+inline bool chain_bounded(const blt_bpe* h) { return h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1; }
+// Sparse passes per run_sparse call (one counter pair each, zeroed once; a longer tail goes back to
+// the full passes).  Counter words: [0] overflow flag, [1] compaction ticket, [2 + p] pass p's seeds,
+// [2 + kSparseMaxPasses + 1 + p] pass p's merges.
+constexpr uint32_t kSparseMaxPasses = 250;
+constexpr uint32_t kSparseCtrWords = 2 + 2 * (kSparseMaxPasses + 1);
 // Chain block of a general map (right after pass 1's status words): u64 pass totals [2], u32 done
 // word, u32 fused-fail word, u64 final total, u32 finish-gate word, pad.
 constexpr uint64_t kChainBlock = 48;
@@ -587,7 +599,8 @@ constexpr uint64_t kChainBlock = 48;
 // general map the pass totals and done flag, two chunk-offset arrays (the passes alternate) and
 // the chunk map of the u16 scan kernel (one word per kTokRange tokens).  The u16 passes run in
 // place in the caller's output.
-WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
+WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
+    const bool single_pass = h->single_pass;
     WsLayout L{};
     const uint64_t tile = single_pass ? std::min<uint64_t>(blt::kTilePos, blt::kTilePosBytes)
                                       : std::min<uint64_t>(blt::kTilePosTok, blt::kTilePosBytes);
@@ -605,6 +618,23 @@ WsLayout ws_layout(bool single_pass, uint64_t n, uint64_t cs) {
     L.stat2 = L.gstat + up16(8 * L.nchunks);   // chain launches: the second status area, per token tile
     L.pctr = L.stat2 + up16(8 * L.ntiles);     // chain launches: ticket and emitted counters per pass
     L.bytes = single_pass ? L.cmap : L.pctr + 8ull * blt::kChainMaxPasses;
+    if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
+        const uint64_t bm = up16(4 * ((n + 31) / 32));
+        const uint64_t cap = n / 64 + 4096;
+        const uint64_t sptiles = (n + blt::kSparseTile - 1) / blt::kSparseTile;
+        L.sp_cap = (uint32_t)cap;
+        L.sp_holes = up16(L.bytes);
+        L.sp_cs = L.sp_holes + bm;
+        L.sp_bits0 = L.sp_cs + bm;
+        L.sp_bits1 = L.sp_bits0 + bm;
+        L.sp_seeds0 = L.sp_bits1 + bm;
+        L.sp_seeds1 = L.sp_seeds0 + up16(4 * cap);
+        L.sp_merges = L.sp_seeds1 + up16(4 * cap);
+        L.sp_tileo = L.sp_merges + up16(12 * cap);
+        L.sp_status = L.sp_tileo + up16(8 * sptiles);
+        L.sp_ctr = L.sp_status + up16(8 * sptiles);
+        L.bytes = L.sp_ctr + 4ull * kSparseCtrWords;
+    }
     return L;
 }
 
@@ -823,8 +853,104 @@ int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t pass
     return fail(BLT_E_IO, "%s", sticky_msg.c_str());
 }
 
-// Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
-constexpr uint32_t kMaxBoundedPasses = 64;
+// Sparse passes of a cyclic map (blt::launch_sparse_*; bpe_kernels.hip explains why they are the
+// greedy passes): 0 off, 1 tried once, at the first pass-count read whose last pass merged under 1/16
+// of its tokens, 2 (default) first right after the fused passes 1 + 2 (one more read), 3 (tests) at
+// the first read whatever the last pass merged.  BLT_SPARSE in the environment, or
+// blt_debug_set_sparse, sets it.
+std::atomic<int> g_sparse{getenv("BLT_SPARSE") ? atoi(getenv("BLT_SPARSE")) : 2};
+// Test hook: sparse passes the calling thread's last general-map encode ran (blt_debug_last_sparse):
+// passes | 1 << 16 when they reached the fixpoint, | 1 << 17 when a list overflowed.
+thread_local uint32_t t_last_sparse = 0;
+// Test hook (blt_debug_set_sparse_cap): the lists' capacity clamped (0: the workspace's), to take the
+// not-taken path.
+std::atomic<uint32_t> g_sparse_cap{0};
+
+struct SparseRun {
+    bool taken = false;      // detect found few enough seeds: the passes ran
+    bool complete = false;   // ... to the fixpoint (else the full passes go on from the compaction)
+    uint32_t passes = 0;     // passes enqueued (an upper bound of those that merged)
+};
+
+// After u16 pass k - 1 (N tokens in place in d_out, chunk starts off_in): sparse passes k, k + 1, ...
+// in the hole layout, then the compaction into d_out, off_out and tot[(k + passes - 1) & 1], as the
+// full passes would leave them.  Not taken (nothing written but the workspace) when the first pass
+// has more seeds than the lists hold.
+int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
+               uint8_t* d_out, uint64_t N, uint64_t k, const uint64_t* off_in, uint64_t* off_out, uint64_t* tot,
+               SparseRun* r) {
+    *r = SparseRun{};
+    if (!L.sp_cap || N == 0 || N >= (1ull << 32)) return 0;
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
+    const uint64_t bm = up16(4 * ((N + 31) / 32));
+    HIP_TRY(hipMemsetAsync(ws + L.sp_holes, 0, bm, s));
+    HIP_TRY(hipMemsetAsync(ws + L.sp_cs, 0, bm, s));
+    HIP_TRY(hipMemsetAsync(ws + L.sp_bits1, 0, bm, s));
+    HIP_TRY(hipMemsetAsync(ws + L.sp_tileo, 0, (L.sp_ctr - L.sp_tileo) + 4ull * kSparseCtrWords, s));
+    blt::SparseParams q{};
+    q.tok = reinterpret_cast<uint16_t*>(d_out);
+    q.n = N;
+    q.holes = reinterpret_cast<uint32_t*>(ws + L.sp_holes);
+    q.cstarts = reinterpret_cast<uint32_t*>(ws + L.sp_cs);
+    q.flags = ctr;
+    q.merges = reinterpret_cast<uint32_t*>(ws + L.sp_merges);
+    const uint32_t cap_over = g_sparse_cap.load(std::memory_order_relaxed);
+    q.cap = cap_over ? std::min(cap_over, L.sp_cap) : L.sp_cap;
+    q.hbuckets = t->hbuckets;
+    q.hmul1 = h->hmul1;
+    q.hmul2 = h->hmul2;
+    q.hshift = h->hshift;
+    q.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
+    q.hone = h->hone ? 1u : 0u;
+    q.coff_in = off_in;
+    q.coff_out = off_out;
+    q.nchunks = L.nchunks;
+    q.tile_o = reinterpret_cast<uint64_t*>(ws + L.sp_tileo);
+    q.status = reinterpret_cast<uint64_t*>(ws + L.sp_status);
+    q.ticket = ctr + 1;
+    q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
+    q.sticky = h->sticky.load(std::memory_order_acquire);
+    uint32_t* seeds[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_seeds0), reinterpret_cast<uint32_t*>(ws + L.sp_seeds1)};
+    uint32_t* bits[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_bits0), reinterpret_cast<uint32_t*>(ws + L.sp_bits1)};
+    auto at_pass = [&](uint32_t pp) {   // pass pp's lists and counters
+        q.seeds_in = seeds[pp & 1];
+        q.bits_in = bits[pp & 1];
+        q.nseeds_in = ctr + 2 + pp;
+        q.seeds_out = seeds[(pp + 1) & 1];
+        q.bits_out = bits[(pp + 1) & 1];
+        q.nseeds_out = ctr + 2 + pp + 1;
+        q.nmerges = ctr + 2 + (kSparseMaxPasses + 1) + pp;
+    };
+    at_pass(0);
+    HIP_TRY(blt::launch_sparse_detect(q, s));
+    // the first batch of passes goes with the detect kernel: when its seeds overflow the list
+    // (c[2] > cap, the flag set) every pass is a no-op and the tokens are untouched
+    uint32_t c[kSparseCtrWords];
+    uint32_t pp = 0;
+    bool overflow = false;
+    for (uint32_t batch = 4;; batch = 8) {
+        const uint32_t e = std::min<uint32_t>(pp + batch, kSparseMaxPasses);
+        for (; pp < e; ++pp) {
+            at_pass(pp);
+            HIP_TRY(blt::launch_sparse_pass(q, s));
+        }
+        HIP_TRY(hipMemcpyAsync(c, ctr, 4ull * (2 + pp + 1), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (c[2] > q.cap) return 0;   // not taken
+        r->taken = true;
+        if (c[0]) {
+            overflow = true;
+            break;
+        }
+        if (c[2 + pp] == 0 || pp >= kSparseMaxPasses) break;   // (the seeds of pass pp, the next to run)
+    }
+    r->passes = pp;
+    r->complete = !overflow && c[2 + pp] == 0;
+    q.total = tot + ((k + pp - 1) & 1);
+    HIP_TRY(blt::launch_sparse_compact(q, s));
+    t_last_sparse = pp | (r->complete ? 1u << 16 : 0u) | (overflow ? 1u << 17 : 0u);
+    return 0;
+}
 
 int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
                   uint64_t* d_chunk_off, void* d_ws, size_t ws_bytes, hipStream_t s, uint64_t* out_tokens,
@@ -838,7 +964,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (d_chunk_off) HIP_TRY(hipMemsetAsync(d_chunk_off, 0, sizeof(uint64_t), s));
         return 0;
     }
-    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    const WsLayout L = ws_layout(h, n, cs);
     if (ws_bytes < L.bytes) return fail(BLT_E_INVALID_INPUT, "workspace too small (%zu < %llu)", ws_bytes, (unsigned long long)L.bytes);
     int dev;
     if (int rc = current_device(&dev)) return rc;
@@ -877,7 +1003,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // pass 1's control block and status words and the chain's totals are contiguous: one memset
     // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
     HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + kChainBlock, s));
-    const bool bounded = h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1;
+    const bool bounded = chain_bounded(h);
     // Passes 1 and 2 in one kernel (run_fused) when the bucket table fits in LDS, chunks hold whole
     // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
     // keep the byte pass, which can); its halo fallback is read where the host reads the chain's
@@ -986,7 +1112,11 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         *out_tokens = rec[3];
         return 0;
     }
-    for (int batch = 1;; batch = 4) {
+    // sparse passes: tried once (policy 2: first right after the fused passes, with no pass to run)
+    const int sp_policy = L.sp_cap ? g_sparse.load(std::memory_order_relaxed) : 0;
+    bool sp_tried = sp_policy == 0;
+    t_last_sparse = 0;
+    for (int batch = (sp_policy == 2 && fused) ? 0 : 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             if (const uint64_t np = chain_len(k, (uint64_t)(batch - b)); np >= 2) {
                 if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
@@ -1013,6 +1143,27 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (fused && (rec[2] >> 32)) return fallback();
         if ((uint32_t)rec[2]) break;
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
+        // the last pass k - 1 left N tokens out of Nin (Nin unknown after the fused passes)
+        const uint64_t N = rec[(k - 1) & 1], Nin = (k >= 3 || !fused) ? rec[k & 1] : 0;
+        if (!sp_tried && (batch == 0 || sp_policy == 3 || (Nin >= N && (Nin - N) * 16 < N))) {
+            sp_tried = true;
+            SparseRun r;
+            if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, N, k, off[cur], off[cur ^ 1], tot, &r)) return rc;
+            if (r.taken) {
+                cur ^= 1;
+                k += r.passes;
+                HIP_TRY(hipMemcpyAsync(rec, tot, 16, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
+                if (r.complete) {
+                    t_last_u16_passes = (uint32_t)(k - 1);
+                    if (d_chunk_off && off[cur] != d_chunk_off)
+                        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+                    if (out_tokens) *out_tokens = rec[(k - 1) & 1];
+                    return 0;
+                }
+            }
+        }
     }
     const uint32_t kdone = (uint32_t)rec[2] & ~blt::kDoneBytePass;   // 0: pass 1 was final
     t_last_u16_passes = kdone;
@@ -1110,7 +1261,7 @@ int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uin
     DevCtx* c = ctx_acquire(dev);
     if (!c) return fail(BLT_E_IO, "cannot create a HIP stream on device %d", dev);
     CtxGuard guard{c};
-    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    const WsLayout L = ws_layout(h, n, cs);
     if (int rc = grow(&c->d_in, &c->in_cap, up16(n))) return rc;
     if (int rc = grow(&c->d_out, &c->out_cap, up16(2 * n))) return rc;
     if (int rc = grow(&c->d_ws, &c->ws_cap, L.bytes)) return rc;
@@ -1134,7 +1285,7 @@ int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uin
 // pinned record).  Slots are cached with the context for the process lifetime.
 int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs) {
     const uint64_t nch = (win + cs - 1) / cs;
-    const WsLayout L = ws_layout(h->single_pass, win, cs);
+    const WsLayout L = ws_layout(h, win, cs);
     if (!P.stream) HIP_TRY(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
     if (!P.counted) HIP_TRY(hipEventCreateWithFlags(&P.counted, hipEventDisableTiming));
     if (P.win < win || P.ws_bytes < L.bytes || P.nch < nch) {
@@ -1222,7 +1373,7 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
             }
             PipeSlot& P = c->pipe[j % slots];
             const uint64_t b0 = w * win, len = std::min(win, n - b0);
-            const WsLayout L = ws_layout(h->single_pass, len, cs);
+            const WsLayout L = ws_layout(h, len, cs);
             int rc = 0;
             if (hipMemcpyAsync(P.d_in, in + b0, len, hipMemcpyHostToDevice, P.stream) != hipSuccess) {
                 rc = fail(BLT_E_IO, "host-to-device copy failed on device %d", c->device);
@@ -1555,7 +1706,7 @@ int blt_bpe_clear_error(const blt_bpe* h) {
 
 size_t blt_bpe_workspace_size(const blt_bpe* h, uint64_t n, uint64_t cs) {
     if (!h || cs == 0) return 0;
-    return (size_t)ws_layout(h->single_pass, n, cs).bytes;
+    return (size_t)ws_layout(h, n, cs).bytes;
 }
 
 int blt_bpe_encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs, uint8_t* d_out,
@@ -1574,7 +1725,7 @@ int blt_bpe_encode_device_ex(const blt_bpe* h, const uint8_t* d_in, uint64_t n, 
 
 int blt_bpe_workspace_reset(const blt_bpe* h, void* d_ws, uint64_t n, uint64_t cs, void* stream) {
     if (!h || !d_ws || cs == 0) return fail(BLT_E_INVALID_INPUT, "bad argument");
-    const WsLayout L = ws_layout(h->single_pass, n, cs);
+    const WsLayout L = ws_layout(h, n, cs);
     HIP_TRY(hipMemsetAsync(d_ws, 0, L.zero_bytes, (hipStream_t)stream));
     // the status words a BLT_ENCODE_WORKSPACE_ZEROED launch may rely on (it refuses beyond them)
     if (L.ntiles <= 0xFFFFFFFFull)
@@ -1607,6 +1758,9 @@ int blt_debug_byte_mode(const blt_bpe* h) {
 // default) enables them; returns the previous setting.
 int blt_debug_set_finish(int on) { return g_finish.exchange(on ? 1 : 0); }
 int blt_debug_set_chain(int on) { return g_chain.exchange(on ? 1 : 0); }
+int blt_debug_set_sparse(int policy) { return g_sparse.exchange(policy); }
+uint32_t blt_debug_last_sparse(void) { return t_last_sparse; }
+uint32_t blt_debug_set_sparse_cap(uint32_t cap) { return g_sparse_cap.exchange(cap); }
 
 // Not in the public header: a general map's longest merge chain (0: single-pass, or unbounded).
 uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0; }
@@ -1743,7 +1897,7 @@ void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) t
             if (blt::launch_noop(c->pipe[0].stream) == hipSuccess) (void)hipStreamSynchronize(c->pipe[0].stream);
             stamp("code object loaded (first launch)");
         } else {
-            const WsLayout L = ws_layout(h->single_pass, n, cs);
+            const WsLayout L = ws_layout(h, n, cs);
             uint8_t* offp = reinterpret_cast<uint8_t*>(c->d_off);
             if (grow(&c->d_in, &c->in_cap, up16(n)) || grow(&c->d_out, &c->out_cap, up16(2 * n)) ||
                 grow(&c->d_ws, &c->ws_cap, L.bytes) || grow(&offp, &c->off_cap, 8 * (L.nchunks + 1)))

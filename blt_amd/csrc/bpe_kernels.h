@@ -127,6 +127,47 @@ hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipS
 // else k_last) gives *tot_final and, when it wrote off1, the caller's chunk offsets.
 hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const uint64_t* off1, uint64_t* chunk_off,
                               uint64_t nchunks, uint32_t k_last, uint64_t* tot_final, hipStream_t s);
+// Sparse passes of a cyclic general map (round 4): once a chain's passes merge almost nothing, the
+// tokens stay in place and consumed positions are marked in a hole bitmap; each pass runs only the
+// maximal runs of mergeable pairs around the previous pass's new tokens, and one compaction writes the
+// result.  Positions below 2^31.
+struct SparseParams {
+    uint16_t* tok;              // tokens as stored (big-endian u16), positions [0, n), in place
+    uint64_t n;
+    uint32_t* holes;            // bit p: position p was consumed by a merge (n bits)
+    uint32_t* cstarts;          // bit p: position p starts a chunk (n bits)
+    uint32_t* seeds_in;         // this pass's seeds (positions), count *nseeds_in, bitmap bits_in
+    uint32_t* nseeds_in;
+    uint32_t* bits_in;
+    uint32_t* seeds_out;        // the next pass's seeds: live tokens this pass made
+    uint32_t* nseeds_out;
+    uint32_t* bits_out;
+    uint32_t* merges;           // (position, consumed position, value) per merge of this pass
+    uint32_t* nmerges;
+    uint32_t* flags;            // [0]: a list overflowed (this pass is not applied)
+    uint32_t cap;               // entries of each list
+    const uint2* hbuckets;      // the map's bucket table (as PassParams)
+    uint32_t hmul1, hmul2, hshift;
+    uint32_t hbytes, hone;      // table bytes (staged in LDS by the detect kernel up to kHashLdsMax), one-probe table
+    // compaction
+    const uint64_t* coff_in;    // chunk starts (positions of the hole layout), [nchunks]
+    uint64_t* coff_out;         // chunk offsets after compaction, [nchunks + 1]
+    uint64_t nchunks;
+    uint64_t* total;            // tokens after compaction
+    uint64_t* tile_o;           // per compaction tile: holes in it (apply), then tokens before it (scan)
+    uint64_t* status;           // per compaction tile: its input is read (zeroed)
+    uint32_t* ticket;           // compaction tile ticket (zeroed)
+    uint32_t* ctl;              // the chain's control block (error flags)
+    uint32_t* sticky;
+};
+constexpr uint64_t kSparseTile = 16384;   // positions per compaction tile
+// detect: the first pass's seeds (every mergeable pair's first position) into seeds_in / bits_in
+hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s);
+// one pass: regions (reads only; merges and new seeds into lists), then the merges applied and the
+// input seeds' bits cleared
+hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s);
+// the hole layout compacted in place: tokens, chunk offsets, total
+hipError_t launch_sparse_compact(const SparseParams& q, hipStream_t s);
 // An empty kernel: the first launch of any kernel loads the library's code object on the device
 // (the CLI's start-up does it on its helper thread, beside the input's mmap).
 hipError_t launch_noop(hipStream_t s);

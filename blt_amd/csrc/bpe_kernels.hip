@@ -3491,6 +3491,402 @@ hipError_t launch_finish(const PassParams& p, int device, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ===========================================================================================
+// Sparse passes of a cyclic general map (round 4).  After a chain's first u16 passes a cyclic map's
+// passes merge almost nothing (self-valued merges on text: 59,215, 460, 16, 2 merges per 2 MiB over
+// four passes), yet each full pass rewrites every token behind its first merge.  Here the tokens stay
+// in place: a merge writes its value at its first position and marks the consumed one in a hole
+// bitmap, and a pass touches only the maximal runs of mergeable pairs.  Why that is the greedy pass
+// (tokenizer.rs:63-86): a run's first position lands (the pair before it does not merge, or it starts
+// a chunk), and inside a run every pair merges, so the pass merges its pairs from the first position
+// on, alternately; everywhere else every position lands and emits itself.  Which runs: in pass k + 1
+// a mergeable pair has a token pass k made (two tokens both left alone by pass k were next to each
+// other in its input too, and the first landed without merging: the pair was looked up and rejected,
+// or cut at a chunk end), and only a live one (a key component) can be in a key.  So pass k's live
+// new tokens are the seeds of pass k + 1, and the first sparse pass takes every mergeable pair as a
+// seed (sparse_detect_kernel).  A run is processed by the thread of its leftmost seed: walking left,
+// a thread that meets another seed in the run leaves it.  Passes read only (the merges and next seeds
+// go to lists); a second kernel applies the merges, so no thread sees another's writes.  A run ends
+// at the first pair that does not merge, also right after a merge: the greedy walk then lands on the
+// next position anyway, but that position's pair belongs to the next run and its owner.
+// (tools/sparse_sim.py restates these passes sequentially against the oracle.)
+// ===========================================================================================
+__device__ __forceinline__ uint32_t sp_lookup(const SparseParams& q, uint32_t key) {
+    const uint2 x = q.hbuckets[bucket_hash(key, q.hmul1, q.hshift)];
+    const uint2 y = q.hbuckets[bucket_hash(key, q.hmul2, q.hshift)];
+    return (x.x == key ? x.y : 0u) | (y.x == key ? y.y : 0u);
+}
+__device__ __forceinline__ bool sp_bit(const uint32_t* b, uint64_t p) { return ((b[p >> 5] >> (p & 31u)) & 1u) != 0u; }
+__device__ __forceinline__ int64_t sp_prev(const SparseParams& q, int64_t p) {   // previous non-hole, or -1
+    for (--p; p >= 0 && sp_bit(q.holes, (uint64_t)p); --p) {}
+    return p;
+}
+__device__ __forceinline__ uint64_t sp_next(const SparseParams& q, uint64_t p) {   // next non-hole, or n
+    for (++p; p < q.n && sp_bit(q.holes, p); ++p) {}
+    return p;
+}
+__device__ __forceinline__ uint32_t sp_key(const SparseParams& q, uint64_t a, uint64_t b) {
+    return (uint32_t)q.tok[a] | ((uint32_t)q.tok[b] << 16);
+}
+
+// Chunk starts into their bitmap (one thread per chunk; the bitmap zeroed before).
+__global__ __launch_bounds__(256) void sparse_cstart_kernel(SparseParams q) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (c >= q.nchunks) return;
+    const uint64_t p = q.coff_in[c];
+    if (p < q.n) atomicOr(&q.cstarts[p >> 5], 1u << (p & 31u));
+}
+
+// Every position whose pair with the next one is a merge (not across a chunk start): the first
+// sparse pass's seeds.  A lane takes 32 aligned positions (64 bytes of tokens, one word of the seed
+// bitmap, stored whole; the next lane's first token and chunk-start bit come by DPP); a wave appends
+// its seeds with one atomic.  The bucket table is staged in LDS when it fits (kLds, dynamic LDS of
+// the table's size): from global memory the lookups' gathers bound the kernel.
+template <bool kLds>
+__global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams q) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    const int lane = threadIdx.x & 63;
+    const uint2* tab = q.hbuckets;
+    if constexpr (kLds) {
+        const uint32_t nw = q.hbytes / 4;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(q.hbuckets);
+        for (uint32_t w = threadIdx.x; w < nw; w += 256) s_dyn[w] = src[w];
+        __syncthreads();
+    }
+    auto lookup = [&](uint32_t key) -> uint32_t {
+        const uint32_t b1 = bucket_hash(key, q.hmul1, q.hshift);
+        const uint2 x = kLds ? reinterpret_cast<const uint2*>(s_dyn)[b1] : tab[b1];
+        uint32_t v = x.x == key ? x.y : 0u;
+        if (!q.hone) {
+            const uint32_t b2 = bucket_hash(key, q.hmul2, q.hshift);
+            const uint2 y = kLds ? reinterpret_cast<const uint2*>(s_dyn)[b2] : tab[b2];
+            v |= y.x == key ? y.y : 0u;
+        }
+        return v;
+    };
+    const uint64_t nwords = (q.n + 31) / 32;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); base < nwords; base += stride) {
+        const uint64_t wd = base + (uint64_t)lane;   // the loop is wave-uniform; lanes past the end add nothing
+        const uint64_t i0 = wd * 32;
+        uint32_t w[16];
+        if (i0 + 32 <= q.n) {
+            const uint4* src = reinterpret_cast<const uint4*>(q.tok + i0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = src[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t lo = i0 + 2u * k < q.n ? q.tok[i0 + 2u * k] : 0u;
+                const uint32_t hi = i0 + 2u * k + 1u < q.n ? q.tok[i0 + 2u * k + 1u] : 0u;
+                w[k] = lo | (hi << 16);
+            }
+        }
+        const uint32_t csw = wd < nwords ? q.cstarts[wd] : 0u;
+        // lane + 1's first token and chunk-start bit (wave_shl:1); lane 63 reads them
+        uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
+        uint32_t nc = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(csw & 1u), 0x130, 0xF, 0xF, false);
+        if (lane == 63) {
+            nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
+            nc = wd + 1 < nwords ? (q.cstarts[wd + 1] & 1u) : 0u;
+        }
+        uint32_t mask = 0;
+        if (wd < nwords) {
+            const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const uint32_t a = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
+                if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
+            }
+            q.bits_in[wd] = mask;
+        }
+        const uint32_t c = __popc(mask);
+        const uint32_t incl = wave_incl_scan(c, lane);
+        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+        if (tot == 0u) continue;   // (uniform)
+        uint32_t b0 = 0;
+        if (lane == 0) b0 = atomicAdd(q.nseeds_in, tot);
+        uint32_t o = (uint32_t)__shfl((int)b0, 0, 64) + incl - c;
+        for (uint32_t m = mask; m; m &= m - 1u, ++o) {
+            if (o < q.cap) q.seeds_in[o] = (uint32_t)(i0 + (uint64_t)__builtin_ctz(m));
+            else atomicOr(q.flags, 1u);
+        }
+    }
+}
+
+// One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.
+__global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams q) {
+    if (*q.flags) return;
+    const uint32_t ns = min(*q.nseeds_in, q.cap);
+    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < ns; idx += gridDim.x * 256u) {
+        const uint64_t sd = q.seeds_in[idx];
+        if (sd >= q.n || sp_bit(q.holes, sd)) continue;   // (never: a seed is a token)
+        uint64_t a = sd;
+        bool owner = true;
+        for (;;) {   // the run's first position
+            if (sp_bit(q.cstarts, a)) break;
+            const int64_t pq = sp_prev(q, (int64_t)a);
+            if (pq < 0 || (sp_lookup(q, sp_key(q, (uint64_t)pq, a)) >> 31) == 0u) break;
+            if (sp_bit(q.bits_in, (uint64_t)pq)) { owner = false; break; }   // an earlier seed owns the run
+            a = (uint64_t)pq;
+        }
+        if (!owner) continue;
+        for (uint64_t i = a;;) {   // greedy from the run's first position, which lands
+            const uint64_t j = sp_next(q, i);
+            if (j >= q.n || sp_bit(q.cstarts, j)) break;
+            const uint32_t v = sp_lookup(q, sp_key(q, i, j));
+            if ((v >> 31) == 0u) break;
+            const uint32_t m = atomicAdd(q.nmerges, 1u);
+            if (m < q.cap) {
+                q.merges[3u * m] = (uint32_t)i;
+                q.merges[3u * m + 1u] = (uint32_t)j;
+                q.merges[3u * m + 2u] = v & 0xFFFFu;
+            } else {
+                atomicOr(q.flags, 1u);
+            }
+            if ((v >> 30) & 1u) {   // a live token: a seed of the next pass
+                const uint32_t so = atomicAdd(q.nseeds_out, 1u);
+                if (so < q.cap) q.seeds_out[so] = (uint32_t)i;
+                else atomicOr(q.flags, 1u);
+                atomicOr(&q.bits_out[i >> 5], 1u << (i & 31u));
+            }
+            const uint64_t k = sp_next(q, j);
+            if (k >= q.n || sp_bit(q.cstarts, k)) break;
+            // k lands; the run goes on only if (j, k) merges: else k starts the next run, whose own
+            // leftmost seed takes it (k's pair may merge, and two threads would both make it)
+            if ((sp_lookup(q, sp_key(q, j, k)) >> 31) == 0u) break;
+            i = k;
+        }
+    }
+}
+
+// The pass's merges applied (unless a list overflowed: then the pass is dropped whole and the host
+// compacts what the earlier passes made), and the pass's seed bits cleared for reuse.
+__global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
+    const uint32_t nm = *q.flags ? 0u : min(*q.nmerges, q.cap);
+    const uint32_t ns = min(*q.nseeds_in, q.cap);
+    const uint32_t nmax = nm > ns ? nm : ns;
+    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < nmax; idx += gridDim.x * 256u) {
+        if (idx < nm) {
+            const uint32_t i = q.merges[3u * idx], j = q.merges[3u * idx + 1u];
+            q.tok[i] = (uint16_t)q.merges[3u * idx + 2u];
+            atomicOr(&q.holes[j >> 5], 1u << (j & 31u));
+            atomicAdd(reinterpret_cast<unsigned long long*>(q.tile_o + j / kSparseTile), 1ull);   // holes per tile
+        }
+        if (idx < ns) {
+            const uint32_t sd = q.seeds_in[idx];
+            atomicAnd(&q.bits_in[sd >> 5], ~(1u << (sd & 31u)));
+        }
+    }
+}
+
+// Compaction of the hole layout in place, in three kernels.  The apply kernels counted each tile's
+// holes; one workgroup scans the counts into every tile's output position (tokens before it).  Then a
+// workgroup per tile (16384 positions: 8-token groups, four per thread, consecutive lanes on
+// consecutive groups) loads its input, stages its tokens in LDS, marks its input read, waits until every earlier tile whose input
+// its output range overlaps has marked its own (the output of tile T lies in [0, end of T's input);
+// with few holes only tile T - 1), and writes the range with 16-byte stores (2-byte ones at the two
+// partial ends, which the neighbouring tiles share).  Tiles come from a ticket, so the tiles waited
+// for are running.
+constexpr int kCpThreads = 512;
+static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
+
+__global__ __launch_bounds__(kCpThreads) void sparse_tile_scan_kernel(SparseParams q) {
+    __shared__ uint64_t s_sum[kCpThreads];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
+    const uint64_t per = (ntiles + kCpThreads - 1) / kCpThreads;
+    const uint64_t t0 = tid * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+    uint64_t h = 0;
+    for (uint64_t t = t0; t < t1; ++t) h += q.tile_o[t];
+    s_sum[tid] = h;
+    __syncthreads();
+    for (uint32_t d = 1; d < (uint32_t)kCpThreads; d <<= 1) {   // Hillis-Steele inclusive scan
+        const uint64_t v = tid >= d ? s_sum[tid - d] : 0ull;
+        __syncthreads();
+        s_sum[tid] += v;
+        __syncthreads();
+    }
+    uint64_t before = s_sum[tid] - h;   // holes before tile t0
+    for (uint64_t t = t0; t < t1; ++t) {
+        const uint64_t c = q.tile_o[t];
+        q.tile_o[t] = t * kSparseTile - before;
+        before += c;
+    }
+    if (tid == kCpThreads - 1) {
+        const uint64_t total = q.n - s_sum[tid];
+        *q.total = total;
+        q.coff_out[q.nchunks] = total;
+    }
+}
+
+__global__ __launch_bounds__(kCpThreads) void sparse_move_kernel(SparseParams q) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile];
+    __shared__ uint32_t s_wsum[4][kCpThreads / 64];
+    __shared__ uint32_t s_T;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
+    if (tid == 0) s_T = atomicAdd(q.ticket, 1u);
+    __syncthreads();
+    const uint64_t T = s_T;
+    if (T >= ntiles) return;   // (uniform; the grid is ntiles workgroups)
+    const uint64_t tile0 = T * kSparseTile, O = q.tile_o[T];
+    // level j: 8-token group G = j * kCpThreads + tid (consecutive lanes read consecutive 16 bytes)
+    uint32_t w[4][4], valid[4], cnt[4], incl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
+        const uint64_t p = tile0 + 8ull * G;
+        valid[j] = 0u;
+        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
+        if (p < q.n) {
+            const uint64_t left = q.n - p;
+            valid[j] = ~(q.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
+            if (left >= 8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(q.tok + p);
+                w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
+            } else {
+                for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)q.tok[p + k] << (16u * (k & 1u));
+            }
+        }
+        cnt[j] = __popc(valid[j]);
+        incl[j] = wave_incl_scan(cnt[j], lane);
+        if (lane == 63) s_wsum[j][wave] = incl[j];
+    }
+    __syncthreads();
+    uint32_t lbase = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t wb = 0, lt = 0;
+#pragma unroll
+        for (int k = 0; k < kCpThreads / 64; ++k) {
+            const uint32_t v = s_wsum[j][k];
+            wb += k < wave ? v : 0u;
+            lt += v;
+        }
+        uint32_t o = lbase + wb + incl[j] - cnt[j];
+        if (valid[j] == 0xFFu) {
+            if ((o & 1u) == 0u) {
+                uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
+                d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s_out[o + k] = (uint16_t)(w[j][k >> 1] >> (16 * (k & 1)));
+            }
+        } else {
+            for (uint32_t m = valid[j]; m; m &= m - 1u, ++o) {
+                const uint32_t k = (uint32_t)__builtin_ctz(m);
+                s_out[o] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
+            }
+        }
+        lbase += lt;
+    }
+    const uint32_t ttot = lbase;
+    __syncthreads();   // every wave has read its input (staged)
+    if (tid == 0) {
+        st_publish(q.status + T, 1ull);
+        const uint64_t next = T + 1 < ntiles ? q.tile_o[T + 1] : *q.total;
+        if (O + ttot != next) flag_error(q.ctl, q.sticky, 4u);   // the hole counts disagree with the bitmap
+    }
+    const uint64_t in_end = tile0 + kSparseTile < q.n ? tile0 + kSparseTile : q.n;
+    if (O == tile0 && ttot == in_end - tile0) return;   // no hole before or in the tile: in place already
+    if (wave == 0) {   // the earlier tiles whose input the output range overlaps
+        bool bad = false;
+        for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < T; u += 64) {
+            SpinClock clk;
+            while (st_read(q.status + u) == 0ull) {
+                if (clk.expired()) { bad = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (__ballot(bad) != 0ull && lane == 0) flag_error(q.ctl, q.sticky, 1u);
+    }
+    __syncthreads();
+    // tokens [O, O + ttot): 8-token groups g0 .. g1 - 1 whole, the ends token by token
+    const uint64_t e = O + ttot, g0 = (O + 7) / 8, g1 = e / 8;
+    if (g0 < g1) {
+        const uint32_t sh = (uint32_t)(8 * g0 - O);   // s_out index of group g0
+        for (uint64_t g = g0 + (uint64_t)tid; g < g1; g += kCpThreads) {
+            const uint32_t b = (uint32_t)(8 * (g - g0)) + sh;
+            uint32_t v[4];
+            if ((sh & 1u) == 0u) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(s_out) + (b >> 1);
+                v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = (uint32_t)s_out[b + 2 * k] | ((uint32_t)s_out[b + 2 * k + 1] << 16);
+            }
+            *reinterpret_cast<uint4*>(q.tok + 8 * g) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        const uint64_t head = sh, tail = e - 8 * g1;   // < 8 each
+        if ((uint64_t)tid < head) q.tok[O + tid] = s_out[tid];
+        else if ((uint64_t)tid >= 8 && (uint64_t)tid < 8 + tail) q.tok[8 * g1 + (tid - 8)] = s_out[8 * g1 - O + (tid - 8)];
+    } else {
+        for (uint64_t k = (uint64_t)tid; k < ttot; k += kCpThreads) q.tok[O + k] = s_out[k];
+    }
+}
+
+// Chunk offsets after the compaction (one wave per chunk): a chunk start (never a hole) moves to its
+// tile's output position plus the tokens of the tile before it.
+__global__ __launch_bounds__(64) void sparse_coff_kernel(SparseParams q) {
+    const uint64_t c = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (c >= q.nchunks) return;
+    const uint64_t p = q.coff_in[c];
+    if (p >= q.n) {   // (never: every chunk holds a token)
+        if (lane == 0) q.coff_out[c] = *q.total;
+        return;
+    }
+    const uint64_t T = p / kSparseTile, wend = p >> 5;
+    uint32_t cnt = 0;
+    for (uint64_t wd = T * (kSparseTile / 32) + (uint64_t)lane; wd < wend; wd += 64) cnt += (uint32_t)__popc(~q.holes[wd]);
+    if (lane == 0) cnt += (uint32_t)__popc(~q.holes[wend] & ((1u << (p & 31u)) - 1u));
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d, 64);
+    if (lane == 0) q.coff_out[c] = q.tile_o[T] + cnt;
+}
+
+// Host check before any sparse launch: every list and bitmap set, positions in 32 bits.
+static bool sparse_ok(const SparseParams& q) {
+    return q.tok && q.holes && q.cstarts && q.seeds_in && q.nseeds_in && q.bits_in && q.seeds_out && q.nseeds_out &&
+           q.bits_out && q.merges && q.nmerges && q.flags && q.cap && q.hbuckets && q.coff_in && q.coff_out &&
+           q.tile_o && q.status && q.ticket && q.n < (1ull << 32);
+}
+hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
+    if (!sparse_ok(q)) return hipErrorInvalidValue;
+    if (q.nchunks) hipLaunchKernelGGL(sparse_cstart_kernel, dim3((unsigned)((q.nchunks + 255) / 256)), dim3(256), 0, s, q);
+    // a lane per 32 positions; every position in one wave of workgroups when the table is small
+    // (each workgroup stages it), else a grid of 2048 looping
+    const uint64_t nwords = (q.n + 31) / 32;
+    uint64_t blocks = (nwords + 255) / 256;
+    const bool lds = q.hbytes && q.hbytes <= kHashLdsMax;
+    if (blocks > 2048 && !(lds && q.hbytes <= 4096)) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    if (lds)
+        hipLaunchKernelGGL(sparse_detect_kernel<true>, dim3((unsigned)blocks), dim3(256), q.hbytes, s, q);
+    else
+        hipLaunchKernelGGL(sparse_detect_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, q);
+    return hipGetLastError();
+}
+hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s) {
+    if (!sparse_ok(q)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sparse_region_kernel, dim3(256), dim3(256), 0, s, q);
+    hipLaunchKernelGGL(sparse_apply_kernel, dim3(256), dim3(256), 0, s, q);
+    return hipGetLastError();
+}
+hipError_t launch_sparse_compact(const SparseParams& q, hipStream_t s) {
+    if (!sparse_ok(q) || !q.total) return hipErrorInvalidValue;
+    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
+    hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(kCpThreads), 0, s, q);
+    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)ntiles), dim3(kCpThreads), 0, s, q);
+    if (q.nchunks) hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q);
+    return hipGetLastError();
+}
+
 __global__ void noop_kernel() {}
 hipError_t launch_noop(hipStream_t s) {
     hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, s);

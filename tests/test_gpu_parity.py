@@ -1123,3 +1123,110 @@ def test_chain_launch_passes(case):
     finally:
         _chain(prev_c)
         _finish(prev_f)
+
+
+def _sparse(policy):
+    return blt_amd._lib.lib().blt_debug_set_sparse(policy)
+
+
+@pytest.mark.parametrize("case", ["selfval_text", "selfval_odd_chunks", "random_cyclic", "random_cyclic_sparse",
+                                  "long_tail", "tail_cut_chunks", "tiny_cap"])
+def test_sparse_passes(case):
+    """Round 4: the sparse passes of a cyclic map (run_sparse: a merge keeps its tokens in place and
+    marks the consumed position in a hole bitmap; a pass walks only the runs of mergeable pairs that
+    hold a seed, the live tokens the pass before made; a compaction in place at the end).  Against
+    the oracle and the full passes (policy 0), tried after the first read of the pass counts (1)
+    and right after the fused passes (2), through the host path and the device API (sync and
+    async, chunk offsets): self-valued merges on text (1 MiB and odd chunks), a random cyclic map, a
+    tail of one merge per run per pass longer than one sparse run takes (the full passes finish
+    it), the same cut by chunk ends, and lists too small for the first pass (not taken)."""
+    import torch
+    import zlib
+    L = blt_amd._lib.lib()
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    cap = 0
+    if case in ("selfval_text", "tiny_cap"):
+        m, cs = synth.SELF_VALUED_MAP, 1 << 20
+        data = synth.text((3 << 20) + 5, seed=17)
+        cap = 8 if case == "tiny_cap" else 0
+    elif case == "selfval_odd_chunks":
+        m, cs = synth.SELF_VALUED_MAP, 65537
+        data = synth.text((2 << 20) + 333, seed=19).copy()
+        for c in range(1, 30):   # 'e' then spaces across chunk starts
+            data[c * cs - 1:c * cs + 3] = (101, 32, 32, 32)
+    elif case == "random_cyclic":
+        m = {}
+        for i, (a, b) in enumerate(rng.integers(97, 101, (10, 2))):
+            m.setdefault((int(a), int(b)), int(rng.integers(97, 101)) if i % 2 else 256 + i)
+        for i in range(12):
+            a, b = int(rng.integers(256, 266)), int(rng.integers(97, 101))
+            m.setdefault((a, b), int(rng.integers(97, 101)))
+        cs = 1 << 17
+        data = rng.integers(97, 101, (1 << 21) + 9, dtype=np.uint8)
+    elif case == "random_cyclic_sparse":   # few mergeable pairs: policy 3 takes the sparse passes early
+        m = {}
+        for i, (a, b) in enumerate(rng.integers(97, 123, (40, 2))):
+            m.setdefault((int(a), int(b)), int(rng.integers(97, 123)) if i % 3 else 256 + i)
+        for i in range(30):
+            a, b = int(rng.integers(256, 296)), int(rng.integers(97, 123))
+            m.setdefault((a, b), int(rng.integers(97, 123)) if i % 2 else 300 + i)
+            m.setdefault((b, a), 256 + (i % 40))
+        cs = 1 << 17
+        data = rng.integers(97, 123, (1 << 21) + 9, dtype=np.uint8)
+    else:                        # (97, 98) -> 97: "ab...b" loses one b per pass
+        m = {(97, 98): 97, (99, 99): 256}
+        parts, size = [], 0
+        while size < (1 << 20):
+            k = int(rng.integers(1, 300)) if rng.random() < 0.02 else int(rng.integers(0, 8))
+            parts.append(np.frombuffer(b"a" + b"b" * k + b"cc" * int(rng.integers(0, 3)), np.uint8))
+            size += parts[-1].size
+        parts.append(np.frombuffer(b"a" + b"b" * 270, np.uint8))
+        data = np.concatenate(parts)
+        cs = 1 << 18 if case == "long_tail" else 4099
+    s = blt_amd.BpeStrategy(m)
+    assert s.info()[1] is False
+    exp, elens = O.COracle(m).run(data, cs, threads=8, return_lens=True)
+    n = data.size
+    nch = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    stream = torch.cuda.current_stream().cuda_stream
+    prev = _sparse(1)
+    prev_cap = L.blt_debug_set_sparse_cap(cap)
+    # chunks of 4099 bytes fit the finish kernels, which would run every pass in LDS
+    prev_f = _finish(case != "tail_cut_chunks")
+    seen = set()
+    try:
+        for policy in (0, 1, 2, 3):
+            _sparse(policy)
+            got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
+            assert np.array_equal(got, exp), (case, policy)
+            assert np.array_equal(lens, elens), (case, policy)
+            for sync in (True, False):
+                d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+                d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+                wsb = s.workspace_size(n, cs)
+                ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+                s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream,
+                                d_off.data_ptr(), sync=sync)
+                torch.cuda.synchronize()
+                if sync:
+                    seen.add((policy, int(L.blt_debug_last_sparse())))
+                offs = d_off.cpu().numpy()
+                assert int(offs[-1]) * 2 == exp.size, (case, policy, sync)
+                assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), (case, policy, sync)
+                assert np.array_equal(np.diff(offs) * 2, elens), (case, policy, sync)
+                s.check_workspace(ws.data_ptr(), stream)
+    finally:
+        _sparse(prev)
+        L.blt_debug_set_sparse_cap(prev_cap)
+        _finish(prev_f)
+    runs = {p: v for p, v in seen}
+    assert runs[0] == 0
+    if case == "tiny_cap":
+        assert runs[2] == 0, runs     # right after the fused passes: more seeds than the lists hold
+    elif case in ("long_tail", "tail_cut_chunks"):
+        assert runs[1] & 0xFFFF == 250 and not runs[1] >> 16, runs   # the full passes finished
+    elif case == "random_cyclic_sparse":
+        assert runs[3] & 0xFFFF > 0, runs                             # taken
+    elif case != "random_cyclic":
+        assert runs[2] >> 16 == 1 and runs[2] & 0xFFFF > 0, runs      # reached the fixpoint

@@ -10,6 +10,7 @@
 #   smoke              __graft_entry__.smoke(), smoke.log
 #   bench              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5, bench.json
 #   bench:ARGS         bench.py with extra arguments (+ for spaces), bench_<n>.json
+#   benche:NAME=VALUE:ARGS  bench.py with one environment setting
 #   benchlib:LIBTAG:ARGS  bench.py on build/exp/libblt_bpe_LIBTAG.so
 #   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/exp/libblt_bpe_LIBTAG.so)
 #   tim:LIBTAG[:ARGS]  tools/tile_timing.py on a timing build (build/exp/libblt_bpe_LIBTAG.so)
@@ -36,7 +37,7 @@ for st in "$@"; do
   case $kind in
     tests)
       # tests[:K] runs only the tests whose names match K (pytest -k; + for spaces)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${a:+-k "${a//+/ }"} \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --durations=8 --timeout 300 --timeout-method thread ${a:+-k "${a//+/ }"} \
         > "$O/tests${a:+_$a}.log" 2>&1 || { tail -40 "$O/tests${a:+_$a}.log"; exit 1; }
       tail -2 "$O/tests${a:+_$a}.log" ;;
     smoke)
@@ -51,6 +52,11 @@ for st in "$@"; do
         timeout -k 10 400 python bench.py ${a//+/ } > "$O/bench_$nb.json" 2> "$O/bench_$nb.err"
         python tools/summarize_bench.py "$O/bench_$nb.json"
       fi ;;
+    benche)
+      # bench.py with one environment setting: benche:NAME=VALUE:ARGS (ARGS + for spaces)
+      nb=$((nb + 1))
+      ( export "$a" && timeout -k 10 400 python bench.py ${b//+/ } > "$O/bench_${a//=/}_$nb.json" 2> "$O/bench_${a//=/}_$nb.err" )
+      echo "[$a]"; python tools/summarize_bench.py "$O/bench_${a//=/}_$nb.json" ;;
     benchlib)
       # bench.py on an experiment build: benchlib:LIBTAG:ARGS (ARGS + for spaces)
       nb=$((nb + 1))
