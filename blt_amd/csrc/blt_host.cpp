@@ -580,7 +580,7 @@ struct WsLayout {
     uint64_t ctl, status, total, off_a, off_b, cmap, gstat, stat2, pctr, bytes, zero_bytes;
     // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
     // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
-    uint64_t sp_holes, sp_cs, sp_bits0, sp_bits1, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr;
+    uint64_t sp_holes, sp_bits0, sp_bits1, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles;
     uint32_t sp_cap;
 };
 // Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
@@ -623,15 +623,15 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
         const uint64_t cap = n / 64 + 4096;
         const uint64_t sptiles = (n + blt::kSparseTile - 1) / blt::kSparseTile;
         L.sp_cap = (uint32_t)cap;
+        L.sp_ntiles = sptiles;
         L.sp_holes = up16(L.bytes);
-        L.sp_cs = L.sp_holes + bm;
-        L.sp_bits0 = L.sp_cs + bm;
+        L.sp_bits0 = L.sp_holes + bm;
         L.sp_bits1 = L.sp_bits0 + bm;
         L.sp_seeds0 = L.sp_bits1 + bm;
         L.sp_seeds1 = L.sp_seeds0 + up16(4 * cap);
         L.sp_merges = L.sp_seeds1 + up16(4 * cap);
         L.sp_tileo = L.sp_merges + up16(12 * cap);
-        L.sp_status = L.sp_tileo + up16(8 * sptiles);
+        L.sp_status = L.sp_tileo + up16(4 * ((sptiles + 15) & ~15ull) + 16);
         L.sp_ctr = L.sp_status + up16(8 * sptiles);
         L.bytes = L.sp_ctr + 4ull * kSparseCtrWords;
     }
@@ -867,31 +867,48 @@ thread_local uint32_t t_last_sparse = 0;
 std::atomic<uint32_t> g_sparse_cap{0};
 
 struct SparseRun {
+    bool gated = false;      // the chain had ended (or the fused kernel must fall back): nothing ran
     bool taken = false;      // detect found few enough seeds: the passes ran
     bool complete = false;   // ... to the fixpoint (else the full passes go on from the compaction)
     uint32_t passes = 0;     // passes enqueued (an upper bound of those that merged)
+    uint64_t rec[4] = {0, 0, 0, 0};   // the chain block's totals, done and fallback words, as read last
+    bool rec_final = false;  // ... read after the compaction
 };
 
-// After u16 pass k - 1 (N tokens in place in d_out, chunk starts off_in): sparse passes k, k + 1, ...
-// in the hole layout, then the compaction into d_out, off_out and tot[(k + passes - 1) & 1], as the
-// full passes would leave them.  Not taken (nothing written but the workspace) when the first pass
-// has more seeds than the lists hold.
+// Host words of the sparse passes' reads (pinned: the reads sit between the device's launches).
+struct SparseHost {
+    uint32_t ctr[kSparseCtrWords];
+    uint64_t rec[4];
+};
+SparseHost* sparse_host() {
+    thread_local SparseHost* p = nullptr;
+    if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(SparseHost), hipHostMallocDefault) != hipSuccess) p = nullptr;
+    return p;
+}
+
+// After u16 pass k - 1 (its token count at n_dev on the device, at most n_max, in place in d_out;
+// chunk starts off_in): sparse passes k, k + 1, ... in the hole layout, then the compaction into
+// d_out, off_out and tot[(k + passes - 1) & 1], as the full passes would leave them.  Enqueued
+// without reading anything first: the detect kernel, four passes and the compaction (which runs only
+// when the four passes reached the fixpoint and detect's seeds fit the lists), then one read of the
+// counters and the chain block.  Passes went on past four: more batches, one read each, then the
+// compaction (the caller reads the totals).  Nothing changes when the gate word (done and fallback
+// words) is set or detect's seeds overflow the lists (not taken).
 int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
-               uint8_t* d_out, uint64_t N, uint64_t k, const uint64_t* off_in, uint64_t* off_out, uint64_t* tot,
-               SparseRun* r) {
+               uint8_t* d_out, const uint64_t* n_dev, uint64_t n_max, const uint64_t* gate, uint64_t k,
+               const uint64_t* off_in, uint64_t* off_out, uint64_t* tot, SparseRun* r) {
     *r = SparseRun{};
-    if (!L.sp_cap || N == 0 || N >= (1ull << 32)) return 0;
+    SparseHost* hb = sparse_host();
+    if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
+    (void)dev;
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
-    const uint64_t bm = up16(4 * ((N + 31) / 32));
-    HIP_TRY(hipMemsetAsync(ws + L.sp_holes, 0, bm, s));
-    HIP_TRY(hipMemsetAsync(ws + L.sp_cs, 0, bm, s));
-    HIP_TRY(hipMemsetAsync(ws + L.sp_bits1, 0, bm, s));
     HIP_TRY(hipMemsetAsync(ws + L.sp_tileo, 0, (L.sp_ctr - L.sp_tileo) + 4ull * kSparseCtrWords, s));
     blt::SparseParams q{};
     q.tok = reinterpret_cast<uint16_t*>(d_out);
-    q.n = N;
+    q.n = n_max;
+    q.n_dev = n_dev;
+    q.gate = gate;
     q.holes = reinterpret_cast<uint32_t*>(ws + L.sp_holes);
-    q.cstarts = reinterpret_cast<uint32_t*>(ws + L.sp_cs);
     q.flags = ctr;
     q.merges = reinterpret_cast<uint32_t*>(ws + L.sp_merges);
     const uint32_t cap_over = g_sparse_cap.load(std::memory_order_relaxed);
@@ -905,7 +922,8 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.coff_in = off_in;
     q.coff_out = off_out;
     q.nchunks = L.nchunks;
-    q.tile_o = reinterpret_cast<uint64_t*>(ws + L.sp_tileo);
+    q.tile_cnt = reinterpret_cast<uint32_t*>(ws + L.sp_tileo);   // (8 B per tile: the counts padded to 16, the total)
+    q.super_cnt = q.tile_cnt + ((L.sp_ntiles + 15) & ~15ull);
     q.status = reinterpret_cast<uint64_t*>(ws + L.sp_status);
     q.ticket = ctr + 1;
     q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
@@ -921,33 +939,52 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
         q.nseeds_out = ctr + 2 + pp + 1;
         q.nmerges = ctr + 2 + (kSparseMaxPasses + 1) + pp;
     };
+    const uint32_t* nseeds0 = ctr + 2;
     at_pass(0);
     HIP_TRY(blt::launch_sparse_detect(q, s));
-    // the first batch of passes goes with the detect kernel: when its seeds overflow the list
-    // (c[2] > cap, the flag set) every pass is a no-op and the tokens are untouched
-    uint32_t c[kSparseCtrWords];
+    constexpr uint32_t kFirst = 4;
     uint32_t pp = 0;
-    bool overflow = false;
-    for (uint32_t batch = 4;; batch = 8) {
-        const uint32_t e = std::min<uint32_t>(pp + batch, kSparseMaxPasses);
+    for (; pp < kFirst; ++pp) {
+        at_pass(pp);
+        HIP_TRY(blt::launch_sparse_pass(q, s));
+    }
+    q.cond = ctr + 2 + kFirst;   // pass kFirst's seeds: none = the fixpoint
+    q.total = tot + ((k + kFirst - 1) & 1);
+    HIP_TRY(blt::launch_sparse_compact(q, nseeds0, s));
+    uint32_t* c = hb->ctr;
+    HIP_TRY(hipMemcpyAsync(c, ctr, 4ull * (2 + kFirst + 1), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hb->rec, tot, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::copy(hb->rec, hb->rec + 4, r->rec);
+    if (r->rec[2]) {   // (the gate: done or fallback words)
+        r->gated = true;
+        return 0;
+    }
+    if (c[2] > q.cap) return 0;   // not taken: every kernel after detect returned at once
+    r->taken = true;
+    bool overflow = c[0] != 0;
+    if (c[2 + kFirst] == 0) {   // the compaction ran
+        r->rec_final = true;
+        r->passes = kFirst;
+        r->complete = !overflow;
+        t_last_sparse = kFirst | (r->complete ? 1u << 16 : 0u) | (overflow ? 1u << 17 : 0u);
+        return 0;
+    }
+    while (!overflow && c[2 + pp] != 0 && pp < kSparseMaxPasses) {   // (the seeds of pass pp, the next to run)
+        const uint32_t e = std::min<uint32_t>(pp + 8, kSparseMaxPasses);
         for (; pp < e; ++pp) {
             at_pass(pp);
             HIP_TRY(blt::launch_sparse_pass(q, s));
         }
         HIP_TRY(hipMemcpyAsync(c, ctr, 4ull * (2 + pp + 1), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (c[2] > q.cap) return 0;   // not taken
-        r->taken = true;
-        if (c[0]) {
-            overflow = true;
-            break;
-        }
-        if (c[2 + pp] == 0 || pp >= kSparseMaxPasses) break;   // (the seeds of pass pp, the next to run)
+        overflow = c[0] != 0;
     }
     r->passes = pp;
     r->complete = !overflow && c[2 + pp] == 0;
+    q.cond = nullptr;
     q.total = tot + ((k + pp - 1) & 1);
-    HIP_TRY(blt::launch_sparse_compact(q, s));
+    HIP_TRY(blt::launch_sparse_compact(q, nseeds0, s));
     t_last_sparse = pp | (r->complete ? 1u << 16 : 0u) | (overflow ? 1u << 17 : 0u);
     return 0;
 }
@@ -1112,11 +1149,44 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         *out_tokens = rec[3];
         return 0;
     }
-    // sparse passes: tried once (policy 2: first right after the fused passes, with no pass to run)
+    // sparse passes: tried once (policy 2: right after the fused passes, enqueued behind them)
     const int sp_policy = L.sp_cap ? g_sparse.load(std::memory_order_relaxed) : 0;
     bool sp_tried = sp_policy == 0;
     t_last_sparse = 0;
-    for (int batch = (sp_policy == 2 && fused) ? 0 : 1;; batch = 4) {
+    // a sparse run that was taken: the passes it ran, then the compaction's results, or the end
+    auto sparse_taken = [&](const SparseRun& r, bool* finished) -> int {
+        *finished = false;
+        cur ^= 1;
+        k += r.passes;
+        if (!r.rec_final) {   // (the totals to read)
+            HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        } else {
+            std::copy(r.rec, r.rec + 4, rec);
+        }
+        if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
+        if (!r.complete) return 0;
+        *finished = true;
+        t_last_u16_passes = (uint32_t)(k - 1);
+        if (d_chunk_off && off[cur] != d_chunk_off)
+            HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+        if (out_tokens) *out_tokens = rec[(k - 1) & 1];
+        return 0;
+    };
+    if (sp_policy == 2 && fused) {
+        sp_tried = true;
+        SparseRun r;
+        const uint64_t* gate = reinterpret_cast<const uint64_t*>(done);   // done word | fallback word
+        if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), n, gate, k, off[cur], off[cur ^ 1],
+                                tot, &r))
+            return rc;
+        if (r.taken) {
+            bool fin = false;
+            if (int rc = sparse_taken(r, &fin)) return rc;
+            if (fin) return 0;
+        }
+    }
+    for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             if (const uint64_t np = chain_len(k, (uint64_t)(batch - b)); np >= 2) {
                 if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
@@ -1145,23 +1215,16 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
         // the last pass k - 1 left N tokens out of Nin (Nin unknown after the fused passes)
         const uint64_t N = rec[(k - 1) & 1], Nin = (k >= 3 || !fused) ? rec[k & 1] : 0;
-        if (!sp_tried && (batch == 0 || sp_policy == 3 || (Nin >= N && (Nin - N) * 16 < N))) {
+        if (!sp_tried && (sp_policy >= 2 || (Nin >= N && (Nin - N) * 16 < N))) {
             sp_tried = true;
             SparseRun r;
-            if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, N, k, off[cur], off[cur ^ 1], tot, &r)) return rc;
+            if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), N, nullptr, k, off[cur],
+                                    off[cur ^ 1], tot, &r))
+                return rc;
             if (r.taken) {
-                cur ^= 1;
-                k += r.passes;
-                HIP_TRY(hipMemcpyAsync(rec, tot, 16, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
-                if (r.complete) {
-                    t_last_u16_passes = (uint32_t)(k - 1);
-                    if (d_chunk_off && off[cur] != d_chunk_off)
-                        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
-                    if (out_tokens) *out_tokens = rec[(k - 1) & 1];
-                    return 0;
-                }
+                bool fin = false;
+                if (int rc = sparse_taken(r, &fin)) return rc;
+                if (fin) return 0;
             }
         }
     }

@@ -133,9 +133,11 @@ hipError_t launch_chain_final(const uint64_t* tot, const uint32_t* done, const u
 // result.  Positions below 2^31.
 struct SparseParams {
     uint16_t* tok;              // tokens as stored (big-endian u16), positions [0, n), in place
-    uint64_t n;
+    uint64_t n;                 // an upper bound of the token count (grid sizes)
+    const uint64_t* n_dev;      // the token count, read by every kernel on the device
+    const uint64_t* gate;       // nonzero: the chain is done or must fall back; every kernel returns
+    const uint32_t* cond;       // compaction kernels: run only when *cond == 0 (null: always)
     uint32_t* holes;            // bit p: position p was consumed by a merge (n bits)
-    uint32_t* cstarts;          // bit p: position p starts a chunk (n bits)
     uint32_t* seeds_in;         // this pass's seeds (positions), count *nseeds_in, bitmap bits_in
     uint32_t* nseeds_in;
     uint32_t* bits_in;
@@ -153,8 +155,9 @@ struct SparseParams {
     const uint64_t* coff_in;    // chunk starts (positions of the hole layout), [nchunks]
     uint64_t* coff_out;         // chunk offsets after compaction, [nchunks + 1]
     uint64_t nchunks;
-    uint64_t* total;            // tokens after compaction
-    uint64_t* tile_o;           // per compaction tile: holes in it (apply), then tokens before it (scan)
+    uint64_t* total;            // tokens after compaction (may be the word n_dev points to: written last)
+    uint32_t* tile_cnt;         // per compaction tile: holes in it (apply kernels), then holes before it (scan)
+    uint32_t* super_cnt;        // one word: the holes in all (scan)
     uint64_t* status;           // per compaction tile: its input is read (zeroed)
     uint32_t* ticket;           // compaction tile ticket (zeroed)
     uint32_t* ctl;              // the chain's control block (error flags)
@@ -166,8 +169,9 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s);
 // one pass: regions (reads only; merges and new seeds into lists), then the merges applied and the
 // input seeds' bits cleared
 hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s);
-// the hole layout compacted in place: tokens, chunk offsets, total
-hipError_t launch_sparse_compact(const SparseParams& q, hipStream_t s);
+// the hole layout compacted in place: tokens, chunk offsets, total (nseeds0: the detect kernel's
+// seed count; nothing runs when it overflowed the lists)
+hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0, hipStream_t s);
 // An empty kernel: the first launch of any kernel loads the library's code object on the device
 // (the CLI's start-up does it on its helper thread, beside the input's mmap).
 hipError_t launch_noop(hipStream_t s);

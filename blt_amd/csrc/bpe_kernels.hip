@@ -3529,12 +3529,14 @@ __device__ __forceinline__ uint32_t sp_key(const SparseParams& q, uint64_t a, ui
     return (uint32_t)q.tok[a] | ((uint32_t)q.tok[b] << 16);
 }
 
-// Chunk starts into their bitmap (one thread per chunk; the bitmap zeroed before).
-__global__ __launch_bounds__(256) void sparse_cstart_kernel(SparseParams q) {
-    const uint64_t c = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (c >= q.nchunks) return;
-    const uint64_t p = q.coff_in[c];
-    if (p < q.n) atomicOr(&q.cstarts[p >> 5], 1u << (p & 31u));
+// Every sparse kernel is enqueued without a host read: it returns when the gate word is set (the
+// chain ended, or the fused kernel must fall back) and reads the token count from the device.  The
+// compaction kernels also return when the detect kernel's seeds overflowed (nothing was applied) or
+// when their condition word is nonzero (the passes before them have not converged: the host runs
+// more passes first).
+__device__ __forceinline__ bool sp_gated(const SparseParams& q) { return q.gate && *q.gate != 0ull; }
+__device__ __forceinline__ bool sp_compact_skip(const SparseParams& q, const uint32_t* nseeds0) {
+    return sp_gated(q) || *nseeds0 > q.cap || (q.cond && *q.cond != 0u);
 }
 
 // Every position whose pair with the next one is a merge (not across a chunk start): the first
@@ -3543,8 +3545,11 @@ __global__ __launch_bounds__(256) void sparse_cstart_kernel(SparseParams q) {
 // its seeds with one atomic.  The bucket table is staged in LDS when it fits (kLds, dynamic LDS of
 // the table's size): from global memory the lookups' gathers bound the kernel.
 template <bool kLds>
-__global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams q) {
+__global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    if (sp_gated(qa)) return;
+    SparseParams q = qa;
+    q.n = *qa.n_dev;
     const int lane = threadIdx.x & 63;
     const uint2* tab = q.hbuckets;
     if constexpr (kLds) {
@@ -3585,14 +3590,26 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams q) {
                 w[k] = lo | (hi << 16);
             }
         }
-        const uint32_t csw = wd < nwords ? q.cstarts[wd] : 0u;
-        // lane + 1's first token and chunk-start bit (wave_shl:1); lane 63 reads them
-        uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
-        uint32_t nc = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(csw & 1u), 0x130, 0xF, 0xF, false);
-        if (lane == 63) {
-            nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
-            nc = wd + 1 < nwords ? (q.cstarts[wd + 1] & 1u) : 0u;
+        // the chunk starts in the wave's 2048 positions and the one after (wave-uniform: a binary
+        // search over the sorted chunk starts, then the few in range): this lane's chunk-start
+        // bits, and whether position i0 + 32 starts a chunk
+        const uint64_t W0 = base * 32;
+        uint64_t lo = 0, hi = q.nchunks;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (q.coff_in[mid] < W0) lo = mid + 1;
+            else hi = mid;
         }
+        uint32_t csw = 0, nc = 0;
+        for (uint64_t c = lo; c < q.nchunks; ++c) {
+            const uint64_t p = q.coff_in[c];
+            if (p > W0 + 2048) break;
+            if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
+            nc |= p == i0 + 32 ? 1u : 0u;
+        }
+        // lane + 1's first token (wave_shl:1); lane 63 reads it
+        uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
+        if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
         uint32_t mask = 0;
         if (wd < nwords) {
             const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
@@ -3602,7 +3619,9 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams q) {
                 const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
                 if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
             }
-            q.bits_in[wd] = mask;
+            q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
+            q.bits_out[wd] = 0u;
+            q.holes[wd] = 0u;
         }
         const uint32_t c = __popc(mask);
         const uint32_t incl = wave_incl_scan(c, lane);
@@ -3619,16 +3638,26 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams q) {
 }
 
 // One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.
-__global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams q) {
-    if (*q.flags) return;
+__global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
+    if (sp_gated(qa) || *qa.flags) return;
+    SparseParams q = qa;
+    q.n = *qa.n_dev;
     const uint32_t ns = min(*q.nseeds_in, q.cap);
     for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < ns; idx += gridDim.x * 256u) {
         const uint64_t sd = q.seeds_in[idx];
         if (sd >= q.n || sp_bit(q.holes, sd)) continue;   // (never: a seed is a token)
+        // the seed's chunk [c0, c1): the last chunk start <= sd (binary search over the sorted starts)
+        uint64_t lo = 0, hi = q.nchunks;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (q.coff_in[mid] <= sd) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t c0 = q.coff_in[lo], c1 = lo + 1 < q.nchunks ? q.coff_in[lo + 1] : q.n;
         uint64_t a = sd;
         bool owner = true;
         for (;;) {   // the run's first position
-            if (sp_bit(q.cstarts, a)) break;
+            if (a == c0) break;
             const int64_t pq = sp_prev(q, (int64_t)a);
             if (pq < 0 || (sp_lookup(q, sp_key(q, (uint64_t)pq, a)) >> 31) == 0u) break;
             if (sp_bit(q.bits_in, (uint64_t)pq)) { owner = false; break; }   // an earlier seed owns the run
@@ -3637,7 +3666,7 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams q) {
         if (!owner) continue;
         for (uint64_t i = a;;) {   // greedy from the run's first position, which lands
             const uint64_t j = sp_next(q, i);
-            if (j >= q.n || sp_bit(q.cstarts, j)) break;
+            if (j >= c1) break;
             const uint32_t v = sp_lookup(q, sp_key(q, i, j));
             if ((v >> 31) == 0u) break;
             const uint32_t m = atomicAdd(q.nmerges, 1u);
@@ -3655,7 +3684,7 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams q) {
                 atomicOr(&q.bits_out[i >> 5], 1u << (i & 31u));
             }
             const uint64_t k = sp_next(q, j);
-            if (k >= q.n || sp_bit(q.cstarts, k)) break;
+            if (k >= c1) break;
             // k lands; the run goes on only if (j, k) merges: else k starts the next run, whose own
             // leftmost seed takes it (k's pair may merge, and two threads would both make it)
             if ((sp_lookup(q, sp_key(q, j, k)) >> 31) == 0u) break;
@@ -3667,6 +3696,7 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams q) {
 // The pass's merges applied (unless a list overflowed: then the pass is dropped whole and the host
 // compacts what the earlier passes made), and the pass's seed bits cleared for reuse.
 __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
+    if (sp_gated(q)) return;
     const uint32_t nm = *q.flags ? 0u : min(*q.nmerges, q.cap);
     const uint32_t ns = min(*q.nseeds_in, q.cap);
     const uint32_t nmax = nm > ns ? nm : ns;
@@ -3675,7 +3705,7 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
             const uint32_t i = q.merges[3u * idx], j = q.merges[3u * idx + 1u];
             q.tok[i] = (uint16_t)q.merges[3u * idx + 2u];
             atomicOr(&q.holes[j >> 5], 1u << (j & 31u));
-            atomicAdd(reinterpret_cast<unsigned long long*>(q.tile_o + j / kSparseTile), 1ull);   // holes per tile
+            atomicAdd(&q.tile_cnt[j / kSparseTile], 1u);   // holes per compaction tile
         }
         if (idx < ns) {
             const uint32_t sd = q.seeds_in[idx];
@@ -3684,181 +3714,248 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
     }
 }
 
-// Compaction of the hole layout in place, in three kernels.  The apply kernels counted each tile's
-// holes; one workgroup scans the counts into every tile's output position (tokens before it).  Then a
-// workgroup per tile (16384 positions: 8-token groups, four per thread, consecutive lanes on
-// consecutive groups) loads its input, stages its tokens in LDS, marks its input read, waits until every earlier tile whose input
+// Compaction of the hole layout in place.  The apply kernels counted the holes per tile of 16384
+// positions; one workgroup scans the counts (a tile's output position is its first position less the
+// holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per tile from a ticket
+// (16384 positions: 8-token groups, four per thread, consecutive lanes on consecutive groups) loads its
+// input, stages its tokens in LDS, marks its input read, waits until every earlier tile whose input
 // its output range overlaps has marked its own (the output of tile T lies in [0, end of T's input);
-// with few holes only tile T - 1), and writes the range with 16-byte stores (2-byte ones at the two
-// partial ends, which the neighbouring tiles share).  Tiles come from a ticket, so the tiles waited
-// for are running.
+// with H holes before it, the ceil(H / 16384) tiles before it), and writes the range with 16-byte
+// stores (2-byte ones at the two partial ends, which the neighbouring tiles share).  Persistent
+// workgroups take tiles from a ticket.
 constexpr int kCpThreads = 512;
 static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
 
-__global__ __launch_bounds__(kCpThreads) void sparse_tile_scan_kernel(SparseParams q) {
-    __shared__ uint64_t s_sum[kCpThreads];
-    const uint32_t tid = threadIdx.x;
+// The tiles' hole counts turned in place into the holes before each tile, and the total into
+// *super_cnt: one workgroup, 16 consecutive counts per thread (four 16-byte loads, lanes on
+// consecutive 64 bytes), rounds of 16384 tiles with the carry between them.
+__global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa, const uint32_t* nseeds0) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    if (sp_compact_skip(qa, nseeds0)) return;
+    SparseParams q = qa;
+    q.n = *qa.n_dev;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
-    const uint64_t per = (ntiles + kCpThreads - 1) / kCpThreads;
-    const uint64_t t0 = tid * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
-    uint64_t h = 0;
-    for (uint64_t t = t0; t < t1; ++t) h += q.tile_o[t];
-    s_sum[tid] = h;
+    const uint64_t nt16 = (ntiles + 15) & ~15ull;   // (the count array is padded: zeroed, 16-byte aligned)
+    if (tid == 0) s_carry = 0u;
     __syncthreads();
-    for (uint32_t d = 1; d < (uint32_t)kCpThreads; d <<= 1) {   // Hillis-Steele inclusive scan
-        const uint64_t v = tid >= d ? s_sum[tid - d] : 0ull;
+    for (uint64_t r0 = 0; r0 < nt16; r0 += 16 * 1024) {
+        const uint64_t t0 = r0 + 16ull * tid;
+        uint32_t c[16];
+        if (t0 < nt16) {
+            const uint4* src = reinterpret_cast<const uint4*>(q.tile_cnt + t0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = src[k];
+                c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = 0u;
+        }
+        uint32_t h = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h += c[k];
+        const uint32_t incl = wave_incl_scan(h, (int)lane);
+        if (lane == 63) s_w[wave] = incl;
         __syncthreads();
-        s_sum[tid] += v;
+        uint32_t before = s_carry, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t v = s_w[k];
+            before += k < wave ? v : 0u;
+            tot += v;
+        }
+        before += incl - h;
+        if (t0 < nt16) {
+            uint32_t o[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                o[k] = before;
+                before += c[k];
+            }
+            uint4* dst = reinterpret_cast<uint4*>(q.tile_cnt + t0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        }
+        __syncthreads();   // (s_w and s_carry read)
+        if (tid == 0) s_carry += tot;
         __syncthreads();
     }
-    uint64_t before = s_sum[tid] - h;   // holes before tile t0
-    for (uint64_t t = t0; t < t1; ++t) {
-        const uint64_t c = q.tile_o[t];
-        q.tile_o[t] = t * kSparseTile - before;
-        before += c;
+    if (tid == 0) *q.super_cnt = s_carry;
+}
+
+__global__ __launch_bounds__(kCpThreads) void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
+    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile];
+    __shared__ uint32_t s_wsum[4][kCpThreads / 64];
+    __shared__ uint32_t s_T[2];
+    if (sp_compact_skip(qa, nseeds0)) return;
+    SparseParams q = qa;
+    q.n = *qa.n_dev;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
+    // level j: 8-token group G = j * kCpThreads + tid (consecutive lanes read consecutive 16 bytes)
+    uint32_t w[4][4], valid[4];
+    auto load_tile = [&](uint64_t TT) {
+        const uint64_t t0 = TT * kSparseTile;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
+            const uint64_t p = t0 + 8ull * G;
+            valid[j] = 0u;
+            w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
+            if (p < q.n) {
+                const uint64_t left = q.n - p;
+                valid[j] = ~(q.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
+                if (left >= 8) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(q.tok + p);
+                    w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
+                } else {
+                    for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)q.tok[p + k] << (16u * (k & 1u));
+                }
+            }
+        }
+    };
+    if (tid == 0) s_T[0] = atomicAdd(q.ticket, 1u);
+    __syncthreads();
+    uint64_t T = s_T[0];
+    if (T < ntiles) load_tile(T);
+    bool first = true;
+    // Persistent, software-pipelined: the next tile's ticket is taken and its input loaded while this
+    // one is staged and written, and it is marked read as soon as its loads are done.  A claimed tile
+    // is loaded by a workgroup that waits only for lower tiles' reads, so the lowest tile in
+    // progress never waits for an unread one.
+    for (uint32_t it = 1; T < ntiles; ++it) {
+        if (tid == 0) s_T[it & 1] = atomicAdd(q.ticket, 1u);
+        const uint64_t tile0 = T * kSparseTile;
+        const uint32_t hb = q.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
+        const uint32_t hnext = T + 1 < ntiles ? q.tile_cnt[T + 1] : *q.super_cnt;
+        const uint64_t O = tile0 - hb;
+        uint32_t cnt[4], incl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cnt[j] = __popc(valid[j]);
+            incl[j] = wave_incl_scan(cnt[j], lane);
+            if (lane == 63) s_wsum[j][wave] = incl[j];
+        }
+        __syncthreads();
+        uint32_t lbase = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t wb = 0, lt = 0;
+#pragma unroll
+            for (int k = 0; k < kCpThreads / 64; ++k) {
+                const uint32_t v = s_wsum[j][k];
+                wb += k < wave ? v : 0u;
+                lt += v;
+            }
+            uint32_t o = lbase + wb + incl[j] - cnt[j];
+            if (valid[j] == 0xFFu) {
+                if ((o & 1u) == 0u) {
+                    uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
+                    d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s_out[o + k] = (uint16_t)(w[j][k >> 1] >> (16 * (k & 1)));
+                }
+            } else {
+                for (uint32_t m = valid[j]; m; m &= m - 1u, ++o) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(m);
+                    s_out[o] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
+                }
+            }
+            lbase += lt;
+        }
+        const uint32_t ttot = lbase;
+        const uint64_t in_end = tile0 + kSparseTile < q.n ? tile0 + kSparseTile : q.n;
+        __syncthreads();   // staged; the next ticket visible
+        const uint64_t Tn = s_T[it & 1];
+        if (tid == 0) {
+            if (first) st_publish(q.status + T, 1ull);   // (later tiles were marked when their loads ended)
+            if (ttot != (in_end - tile0) - (hnext - hb)) flag_error(q.ctl, q.sticky, 4u);   // counts vs bitmap
+        }
+        first = false;
+        const bool moves = !(O == tile0 && ttot == in_end - tile0);   // else in place already (uniform)
+        if (moves) {
+            if (wave == 0) {   // the earlier tiles whose input the output range overlaps
+                bool bad = false;
+                for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < T; u += 64) {
+                    SpinClock clk;
+                    while (st_read(q.status + u) == 0ull) {
+                        if (clk.expired()) { bad = true; break; }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                if (__ballot(bad) != 0ull && lane == 0) flag_error(q.ctl, q.sticky, 1u);
+            }
+            __syncthreads();
+        }
+        if (Tn < ntiles) load_tile(Tn);   // the next tile's loads go out ahead of this tile's stores
+        if (moves) {
+            // tokens [O, O + ttot): 8-token groups g0 .. g1 - 1 whole, the ends token by token
+            const uint64_t e = O + ttot, g0 = (O + 7) / 8, g1 = e / 8;
+            if (g0 < g1) {
+                const uint32_t sh = (uint32_t)(8 * g0 - O);   // s_out index of group g0
+                for (uint64_t g = g0 + (uint64_t)tid; g < g1; g += kCpThreads) {
+                    const uint32_t b = (uint32_t)(8 * (g - g0)) + sh;
+                    uint32_t v[4];
+                    if ((sh & 1u) == 0u) {
+                        const uint32_t* src = reinterpret_cast<const uint32_t*>(s_out) + (b >> 1);
+                        v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) v[k] = (uint32_t)s_out[b + 2 * k] | ((uint32_t)s_out[b + 2 * k + 1] << 16);
+                    }
+                    *reinterpret_cast<uint4*>(q.tok + 8 * g) = make_uint4(v[0], v[1], v[2], v[3]);
+                }
+                const uint64_t head = sh, tail = e - 8 * g1;   // < 8 each
+                if ((uint64_t)tid < head) q.tok[O + tid] = s_out[tid];
+                else if ((uint64_t)tid >= 8 && (uint64_t)tid < 8 + tail) q.tok[8 * g1 + (tid - 8)] = s_out[8 * g1 - O + (tid - 8)];
+            } else {
+                for (uint64_t k = (uint64_t)tid; k < ttot; k += kCpThreads) q.tok[O + k] = s_out[k];
+            }
+        }
+        // the next tile's input is in registers once this wave's loads are done (its stores too: one
+        // counter); after the barrier every wave's are, and the tile is marked read
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();   // (s_out and s_wsum free again)
+        if (tid == 0 && Tn < ntiles) st_publish(q.status + Tn, 1ull);
+        T = Tn;
     }
-    if (tid == kCpThreads - 1) {
-        const uint64_t total = q.n - s_sum[tid];
+}
+
+// Chunk offsets after the compaction (one wave per chunk): a chunk start (never a hole) moves left by
+// the holes before it.  Block 0 also writes the total, to a word that may be the one the count came
+// from (no other kernel here reads the count after this one starts).
+__global__ __launch_bounds__(64) void sparse_coff_kernel(SparseParams q, const uint32_t* nseeds0) {
+    const uint64_t c = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (c >= q.nchunks || sp_compact_skip(q, nseeds0)) return;
+    if (c == 0 && lane == 0) {
+        const uint64_t total = *q.n_dev - *q.super_cnt;
         *q.total = total;
         q.coff_out[q.nchunks] = total;
     }
-}
-
-__global__ __launch_bounds__(kCpThreads) void sparse_move_kernel(SparseParams q) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile];
-    __shared__ uint32_t s_wsum[4][kCpThreads / 64];
-    __shared__ uint32_t s_T;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
-    if (tid == 0) s_T = atomicAdd(q.ticket, 1u);
-    __syncthreads();
-    const uint64_t T = s_T;
-    if (T >= ntiles) return;   // (uniform; the grid is ntiles workgroups)
-    const uint64_t tile0 = T * kSparseTile, O = q.tile_o[T];
-    // level j: 8-token group G = j * kCpThreads + tid (consecutive lanes read consecutive 16 bytes)
-    uint32_t w[4][4], valid[4], cnt[4], incl[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
-        const uint64_t p = tile0 + 8ull * G;
-        valid[j] = 0u;
-        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
-        if (p < q.n) {
-            const uint64_t left = q.n - p;
-            valid[j] = ~(q.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
-            if (left >= 8) {
-                const uint4 v = *reinterpret_cast<const uint4*>(q.tok + p);
-                w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
-            } else {
-                for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)q.tok[p + k] << (16u * (k & 1u));
-            }
-        }
-        cnt[j] = __popc(valid[j]);
-        incl[j] = wave_incl_scan(cnt[j], lane);
-        if (lane == 63) s_wsum[j][wave] = incl[j];
-    }
-    __syncthreads();
-    uint32_t lbase = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t wb = 0, lt = 0;
-#pragma unroll
-        for (int k = 0; k < kCpThreads / 64; ++k) {
-            const uint32_t v = s_wsum[j][k];
-            wb += k < wave ? v : 0u;
-            lt += v;
-        }
-        uint32_t o = lbase + wb + incl[j] - cnt[j];
-        if (valid[j] == 0xFFu) {
-            if ((o & 1u) == 0u) {
-                uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
-                d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s_out[o + k] = (uint16_t)(w[j][k >> 1] >> (16 * (k & 1)));
-            }
-        } else {
-            for (uint32_t m = valid[j]; m; m &= m - 1u, ++o) {
-                const uint32_t k = (uint32_t)__builtin_ctz(m);
-                s_out[o] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
-            }
-        }
-        lbase += lt;
-    }
-    const uint32_t ttot = lbase;
-    __syncthreads();   // every wave has read its input (staged)
-    if (tid == 0) {
-        st_publish(q.status + T, 1ull);
-        const uint64_t next = T + 1 < ntiles ? q.tile_o[T + 1] : *q.total;
-        if (O + ttot != next) flag_error(q.ctl, q.sticky, 4u);   // the hole counts disagree with the bitmap
-    }
-    const uint64_t in_end = tile0 + kSparseTile < q.n ? tile0 + kSparseTile : q.n;
-    if (O == tile0 && ttot == in_end - tile0) return;   // no hole before or in the tile: in place already
-    if (wave == 0) {   // the earlier tiles whose input the output range overlaps
-        bool bad = false;
-        for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < T; u += 64) {
-            SpinClock clk;
-            while (st_read(q.status + u) == 0ull) {
-                if (clk.expired()) { bad = true; break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        if (__ballot(bad) != 0ull && lane == 0) flag_error(q.ctl, q.sticky, 1u);
-    }
-    __syncthreads();
-    // tokens [O, O + ttot): 8-token groups g0 .. g1 - 1 whole, the ends token by token
-    const uint64_t e = O + ttot, g0 = (O + 7) / 8, g1 = e / 8;
-    if (g0 < g1) {
-        const uint32_t sh = (uint32_t)(8 * g0 - O);   // s_out index of group g0
-        for (uint64_t g = g0 + (uint64_t)tid; g < g1; g += kCpThreads) {
-            const uint32_t b = (uint32_t)(8 * (g - g0)) + sh;
-            uint32_t v[4];
-            if ((sh & 1u) == 0u) {
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(s_out) + (b >> 1);
-                v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) v[k] = (uint32_t)s_out[b + 2 * k] | ((uint32_t)s_out[b + 2 * k + 1] << 16);
-            }
-            *reinterpret_cast<uint4*>(q.tok + 8 * g) = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        const uint64_t head = sh, tail = e - 8 * g1;   // < 8 each
-        if ((uint64_t)tid < head) q.tok[O + tid] = s_out[tid];
-        else if ((uint64_t)tid >= 8 && (uint64_t)tid < 8 + tail) q.tok[8 * g1 + (tid - 8)] = s_out[8 * g1 - O + (tid - 8)];
-    } else {
-        for (uint64_t k = (uint64_t)tid; k < ttot; k += kCpThreads) q.tok[O + k] = s_out[k];
-    }
-}
-
-// Chunk offsets after the compaction (one wave per chunk): a chunk start (never a hole) moves to its
-// tile's output position plus the tokens of the tile before it.
-__global__ __launch_bounds__(64) void sparse_coff_kernel(SparseParams q) {
-    const uint64_t c = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (c >= q.nchunks) return;
-    const uint64_t p = q.coff_in[c];
-    if (p >= q.n) {   // (never: every chunk holds a token)
-        if (lane == 0) q.coff_out[c] = *q.total;
-        return;
-    }
+    const uint64_t p = q.coff_in[c];   // (< the count: every chunk holds a token)
     const uint64_t T = p / kSparseTile, wend = p >> 5;
+    const uint32_t hb = q.tile_cnt[T];
     uint32_t cnt = 0;
     for (uint64_t wd = T * (kSparseTile / 32) + (uint64_t)lane; wd < wend; wd += 64) cnt += (uint32_t)__popc(~q.holes[wd]);
     if (lane == 0) cnt += (uint32_t)__popc(~q.holes[wend] & ((1u << (p & 31u)) - 1u));
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d, 64);
-    if (lane == 0) q.coff_out[c] = q.tile_o[T] + cnt;
+    if (lane == 0) q.coff_out[c] = T * kSparseTile - hb + cnt;
 }
 
 // Host check before any sparse launch: every list and bitmap set, positions in 32 bits.
 static bool sparse_ok(const SparseParams& q) {
-    return q.tok && q.holes && q.cstarts && q.seeds_in && q.nseeds_in && q.bits_in && q.seeds_out && q.nseeds_out &&
+    return q.tok && q.n_dev && q.holes && q.seeds_in && q.nseeds_in && q.bits_in && q.seeds_out && q.nseeds_out &&
            q.bits_out && q.merges && q.nmerges && q.flags && q.cap && q.hbuckets && q.coff_in && q.coff_out &&
-           q.tile_o && q.status && q.ticket && q.n < (1ull << 32);
+           q.tile_cnt && q.super_cnt && q.status && q.ticket && q.n < (1ull << 32);
 }
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
-    if (q.nchunks) hipLaunchKernelGGL(sparse_cstart_kernel, dim3((unsigned)((q.nchunks + 255) / 256)), dim3(256), 0, s, q);
     // a lane per 32 positions; every position in one wave of workgroups when the table is small
     // (each workgroup stages it), else a grid of 2048 looping
     const uint64_t nwords = (q.n + 31) / 32;
@@ -3878,12 +3975,14 @@ hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s) {
     hipLaunchKernelGGL(sparse_apply_kernel, dim3(256), dim3(256), 0, s, q);
     return hipGetLastError();
 }
-hipError_t launch_sparse_compact(const SparseParams& q, hipStream_t s) {
-    if (!sparse_ok(q) || !q.total) return hipErrorInvalidValue;
+hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0, hipStream_t s) {
+    if (!sparse_ok(q) || !q.total || !nseeds0 || !q.nchunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
-    hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(kCpThreads), 0, s, q);
-    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)ntiles), dim3(kCpThreads), 0, s, q);
-    if (q.nchunks) hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q);
+    hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(1024), 0, s, q, nseeds0);
+    // persistent: four workgroups per CU (32 KiB of LDS each)
+    const uint64_t grid = ntiles < 1024 ? ntiles : 1024;
+    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)grid), dim3(kCpThreads), 0, s, q, nseeds0);
+    hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q, nseeds0);
     return hipGetLastError();
 }
 
