@@ -580,7 +580,7 @@ struct WsLayout {
     uint64_t ctl, status, total, off_a, off_b, cmap, gstat, stat2, pctr, bytes, zero_bytes;
     // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
     // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
-    uint64_t sp_holes, sp_bits0, sp_bits1, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles;
+    uint64_t sp_holes, sp_bits0, sp_bits1, sp_bits2, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles;
     uint32_t sp_cap;
 };
 // Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
@@ -620,14 +620,15 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
     L.bytes = single_pass ? L.cmap : L.pctr + 8ull * blt::kChainMaxPasses;
     if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
         const uint64_t bm = up16(4 * ((n + 31) / 32));
-        const uint64_t cap = n / 64 + 4096;
+        const uint64_t cap = n / 16 + 4096;
         const uint64_t sptiles = (n + blt::kSparseTile - 1) / blt::kSparseTile;
         L.sp_cap = (uint32_t)cap;
         L.sp_ntiles = sptiles;
         L.sp_holes = up16(L.bytes);
         L.sp_bits0 = L.sp_holes + bm;
         L.sp_bits1 = L.sp_bits0 + bm;
-        L.sp_seeds0 = L.sp_bits1 + bm;
+        L.sp_bits2 = L.sp_bits1 + bm;
+        L.sp_seeds0 = L.sp_bits2 + bm;
         L.sp_seeds1 = L.sp_seeds0 + up16(4 * cap);
         L.sp_merges = L.sp_seeds1 + up16(4 * cap);
         L.sp_tileo = L.sp_merges + up16(12 * cap);
@@ -854,11 +855,16 @@ int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t pass
 }
 
 // Sparse passes of a cyclic map (blt::launch_sparse_*; bpe_kernels.hip explains why they are the
-// greedy passes): 0 off, 1 tried once, at the first pass-count read whose last pass merged under 1/16
-// of its tokens, 2 (default) first right after the fused passes 1 + 2 (one more read), 3 (tests) at
-// the first read whatever the last pass merged.  BLT_SPARSE in the environment, or
-// blt_debug_set_sparse, sets it.
-std::atomic<int> g_sparse{getenv("BLT_SPARSE") ? atoi(getenv("BLT_SPARSE")) : 2};
+// greedy passes), tried once per encode:
+//   0 off;
+//   1 at the first pass-count read whose last pass merged under 1/16 of its tokens;
+//   2 enqueued right behind the fused passes 1 + 2, then as 3;
+//   3 (tests) at the first pass-count read, whatever the last pass merged;
+//   4 (default) enqueued right behind the byte pass (no fused kernel), for maps whose byte pass cannot
+//     end the chain (the others as 3).  On selfval (256 MiB): 0.85 ms against 1.01 with 2 and 1.34
+//     with 0: the byte pass and one sparse first pass (7.6 M merges) cost less than the fused kernel.
+// BLT_SPARSE in the environment, or blt_debug_set_sparse, sets it.
+std::atomic<int> g_sparse{getenv("BLT_SPARSE") ? atoi(getenv("BLT_SPARSE")) : 4};
 // Test hook: sparse passes the calling thread's last general-map encode ran (blt_debug_last_sparse):
 // passes | 1 << 16 when they reached the fixpoint, | 1 << 17 when a list overflowed.
 thread_local uint32_t t_last_sparse = 0;
@@ -929,19 +935,30 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     q.sticky = h->sticky.load(std::memory_order_acquire);
     uint32_t* seeds[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_seeds0), reinterpret_cast<uint32_t*>(ws + L.sp_seeds1)};
-    uint32_t* bits[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_bits0), reinterpret_cast<uint32_t*>(ws + L.sp_bits1)};
+    uint32_t* bits0 = reinterpret_cast<uint32_t*>(ws + L.sp_bits0);
+    uint32_t* bits[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_bits1), reinterpret_cast<uint32_t*>(ws + L.sp_bits2)};
+    // pass p reads list p & 1 (pass 0's from sparse_list_kernel); its seed bitmap is detect's bits0
+    // for pass 0, then bits[(p - 1) & 1], which pass p - 1 wrote (and pass p's apply kernel clears)
     auto at_pass = [&](uint32_t pp) {   // pass pp's lists and counters
         q.seeds_in = seeds[pp & 1];
-        q.bits_in = bits[pp & 1];
+        q.bits_in = pp ? bits[(pp - 1) & 1] : bits0;
         q.nseeds_in = ctr + 2 + pp;
         q.seeds_out = seeds[(pp + 1) & 1];
-        q.bits_out = bits[(pp + 1) & 1];
+        q.bits_out = bits[pp & 1];
+        q.bits_alt = bits[1];
         q.nseeds_out = ctr + 2 + pp + 1;
         q.nmerges = ctr + 2 + (kSparseMaxPasses + 1) + pp;
+        q.first_pass = pp == 0 ? 1u : 0u;
     };
     const uint32_t* nseeds0 = ctr + 2;
     at_pass(0);
     HIP_TRY(blt::launch_sparse_detect(q, s));
+    {   // pass 0's list: bits0 into list 0, counter ctr[2]
+        blt::SparseParams ql = q;
+        ql.seeds_out = seeds[0];
+        ql.nseeds_out = ctr + 2;
+        HIP_TRY(blt::launch_sparse_list(ql, s));
+    }
     constexpr uint32_t kFirst = 4;
     uint32_t pp = 0;
     for (; pp < kFirst; ++pp) {
@@ -960,7 +977,7 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
         r->gated = true;
         return 0;
     }
-    if (c[2] > q.cap) return 0;   // not taken: every kernel after detect returned at once
+    if (c[0] & 2u) return 0;   // not taken: the first pass overflowed the lists, nothing was applied
     r->taken = true;
     bool overflow = c[0] != 0;
     if (c[2 + kFirst] == 0) {   // the compaction ran
@@ -1045,7 +1062,9 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
     // keep the byte pass, which can); its halo fallback is read where the host reads the chain's
     // totals anyway, so an async bounded chain keeps the two-kernel path.
+    const int sp_policy = L.sp_cap ? g_sparse.load(std::memory_order_relaxed) : 0;
     const bool fused = !(flags & kEncodeNoFused) && g_fused.load(std::memory_order_relaxed) && !h->live_first &&
+                       !(sp_policy == 4 && !h->live_first) &&
                        !h->byte_self_pair &&
                        h->hwords.size() * sizeof(uint32_t) <= blt::kHashLdsMax && cs >= blt::kMinChunkBytes &&
                        (!bounded || out_tokens != nullptr);
@@ -1149,8 +1168,8 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         *out_tokens = rec[3];
         return 0;
     }
-    // sparse passes: tried once (policy 2: right after the fused passes, enqueued behind them)
-    const int sp_policy = L.sp_cap ? g_sparse.load(std::memory_order_relaxed) : 0;
+    // sparse passes: tried once (policy 2: right after the fused passes, enqueued behind them;
+    // policy 4: right after the byte pass)
     bool sp_tried = sp_policy == 0;
     t_last_sparse = 0;
     // a sparse run that was taken: the passes it ran, then the compaction's results, or the end
@@ -1173,7 +1192,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (out_tokens) *out_tokens = rec[(k - 1) & 1];
         return 0;
     };
-    if (sp_policy == 2 && fused) {
+    if ((sp_policy == 2 && fused) || (sp_policy == 4 && !fused && !bounded && !h->live_first)) {
         sp_tried = true;
         SparseRun r;
         const uint64_t* gate = reinterpret_cast<const uint64_t*>(done);   // done word | fallback word

@@ -139,11 +139,14 @@ struct SparseParams {
     const uint32_t* cond;       // compaction kernels: run only when *cond == 0 (null: always)
     uint32_t* holes;            // bit p: position p was consumed by a merge (n bits)
     uint32_t* seeds_in;         // this pass's seeds (positions), count *nseeds_in, bitmap bits_in
+                                // (null: the first pass, seeds = the bitmap bits_in)
     uint32_t* nseeds_in;
     uint32_t* bits_in;
     uint32_t* seeds_out;        // the next pass's seeds: live tokens this pass made
     uint32_t* nseeds_out;
     uint32_t* bits_out;
+    uint32_t* bits_alt;         // the later passes' other seed bitmap (the detect kernel zeroes it)
+    uint32_t first_pass;        // 1: the first pass (an overflow leaves everything untouched)
     uint32_t* merges;           // (position, consumed position, value) per merge of this pass
     uint32_t* nmerges;
     uint32_t* flags;            // [0]: a list overflowed (this pass is not applied)
@@ -166,6 +169,8 @@ struct SparseParams {
 constexpr uint64_t kSparseTile = 16384;   // positions per compaction tile
 // detect: the first pass's seeds (every mergeable pair's first position) into seeds_in / bits_in
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s);
+// the first pass's seed list from the detect kernel's bitmap (q.seeds_out, q.nseeds_out)
+hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s);
 // one pass: regions (reads only; merges and new seeds into lists), then the merges applied and the
 // input seeds' bits cleared
 hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s);

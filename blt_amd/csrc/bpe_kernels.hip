@@ -3536,14 +3536,16 @@ __device__ __forceinline__ uint32_t sp_key(const SparseParams& q, uint64_t a, ui
 // more passes first).
 __device__ __forceinline__ bool sp_gated(const SparseParams& q) { return q.gate && *q.gate != 0ull; }
 __device__ __forceinline__ bool sp_compact_skip(const SparseParams& q, const uint32_t* nseeds0) {
-    return sp_gated(q) || *nseeds0 > q.cap || (q.cond && *q.cond != 0u);
+    (void)nseeds0;
+    return sp_gated(q) || (*q.flags & 2u) != 0u || (q.cond && *q.cond != 0u);
 }
 
 // Every position whose pair with the next one is a merge (not across a chunk start): the first
-// sparse pass's seeds.  A lane takes 32 aligned positions (64 bytes of tokens, one word of the seed
-// bitmap, stored whole; the next lane's first token and chunk-start bit come by DPP); a wave appends
-// its seeds with one atomic.  The bucket table is staged in LDS when it fits (kLds, dynamic LDS of
-// the table's size): from global memory the lookups' gathers bound the kernel.
+// sparse pass's seeds, as a bitmap (bits_in; the first pass reads its seeds from it, so no list and
+// no atomics here: appending millions of seeds to one counter serialised on its address, 561 us on
+// selfval's 8 M).  A lane takes 32 aligned positions (64 bytes of tokens, one word of each bitmap,
+// stored whole: the seed bitmap, the holes and the later passes' two seed bitmaps zeroed); the next
+// lane's first token comes by DPP.  The bucket table is staged in LDS when it fits (kLds).
 template <bool kLds>
 __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -3571,7 +3573,7 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     };
     const uint64_t nwords = (q.n + 31) / 32;
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u); base < nwords; base += stride) {
+    for (uint64_t base = (uint64_t)blockIdx.x * 256u + (uint64_t)(threadIdx.x & ~63u); base < nwords; base += stride) {
         const uint64_t wd = base + (uint64_t)lane;   // the loop is wave-uniform; lanes past the end add nothing
         const uint64_t i0 = wd * 32;
         uint32_t w[16];
@@ -3610,8 +3612,8 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
         // lane + 1's first token (wave_shl:1); lane 63 reads it
         uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
         if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
-        uint32_t mask = 0;
         if (wd < nwords) {
+            uint32_t mask = 0;
             const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
 #pragma unroll
             for (int k = 0; k < 32; ++k) {
@@ -3621,74 +3623,162 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
             }
             q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
             q.bits_out[wd] = 0u;
+            q.bits_alt[wd] = 0u;
             q.holes[wd] = 0u;
-        }
-        const uint32_t c = __popc(mask);
-        const uint32_t incl = wave_incl_scan(c, lane);
-        const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
-        if (tot == 0u) continue;   // (uniform)
-        uint32_t b0 = 0;
-        if (lane == 0) b0 = atomicAdd(q.nseeds_in, tot);
-        uint32_t o = (uint32_t)__shfl((int)b0, 0, 64) + incl - c;
-        for (uint32_t m = mask; m; m &= m - 1u, ++o) {
-            if (o < q.cap) q.seeds_in[o] = (uint32_t)(i0 + (uint64_t)__builtin_ctz(m));
-            else atomicOr(q.flags, 1u);
         }
     }
 }
 
-// One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.
+// The first pass's seed list from the detect kernel's bitmap: a workgroup per contiguous range of
+// words counts its seeds, reserves its part of the list with one atomic, then writes the seeds in
+// position order, 256 words at a time (a workgroup scan per round).  A first pass that reads its
+// bitmap directly, a lane per word, measured 549 us on selfval's 8 M seeds against 20 us from this list.
+__global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_base, s_run;
+    if (sp_gated(qa)) return;
+    SparseParams q = qa;
+    q.n = *qa.n_dev;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t nwords = (q.n + 31) / 32;
+    const uint64_t per = ((nwords + gridDim.x - 1) / gridDim.x + 255) & ~255ull;
+    const uint64_t w0 = (uint64_t)blockIdx.x * per, w1 = w0 + per < nwords ? w0 + per : nwords;
+    if (w0 >= w1) return;   // (uniform)
+    uint32_t h = 0;
+    for (uint64_t wd = w0 + tid; wd < w1; wd += 256) h += (uint32_t)__popc(q.bits_in[wd]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) h += (uint32_t)__shfl_xor((int)h, d, 64);
+    if (lane == 0) s_w[wave] = h;
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        s_base = tot ? atomicAdd(q.nseeds_out, tot) : 0u;
+        s_run = 0u;
+    }
+    __syncthreads();
+    const uint32_t base = s_base;
+    for (uint64_t r0 = w0; r0 < w1; r0 += 256) {   // (uniform)
+        const uint64_t wd = r0 + tid;
+        const uint32_t m = wd < w1 ? q.bits_in[wd] : 0u;
+        const uint32_t c = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan(c, (int)lane);
+        __syncthreads();   // (s_w, s_run of the round before read)
+        if (lane == 63) s_w[wave] = incl;
+        __syncthreads();
+        uint32_t o = base + s_run + incl - c;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) o += k < wave ? s_w[k] : 0u;
+        for (uint32_t mm = m; mm; mm &= mm - 1u, ++o) {
+            if (o < q.cap) q.seeds_out[o] = (uint32_t)(32ull * wd + (uint64_t)__builtin_ctz(mm));
+            else atomicOr(q.flags, 3u);
+        }
+        __syncthreads();
+        if (tid == 0) s_run += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    }
+}
+
+// One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.  The first pass
+// takes its seeds from the detect kernel's bitmap (a lane per word: up to 32 seeds each, one after
+// the other), the later ones from the list the pass before made.  A wave takes 64 words or list
+// entries; its lanes walk their runs in step, one merge per lane per step, and each step's merges and
+// new seeds are appended with one atomic per list.  An overflow in the first pass sets flag bit 2:
+// nothing is applied and the compaction does not run (the tokens stay as they were).
 __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
     if (sp_gated(qa) || *qa.flags) return;
     SparseParams q = qa;
     q.n = *qa.n_dev;
-    const uint32_t ns = min(*q.nseeds_in, q.cap);
-    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < ns; idx += gridDim.x * 256u) {
-        const uint64_t sd = q.seeds_in[idx];
-        if (sd >= q.n || sp_bit(q.holes, sd)) continue;   // (never: a seed is a token)
-        // the seed's chunk [c0, c1): the last chunk start <= sd (binary search over the sorted starts)
-        uint64_t lo = 0, hi = q.nchunks;
-        while (hi - lo > 1) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (q.coff_in[mid] <= sd) lo = mid;
-            else hi = mid;
-        }
-        const uint64_t c0 = q.coff_in[lo], c1 = lo + 1 < q.nchunks ? q.coff_in[lo + 1] : q.n;
-        uint64_t a = sd;
-        bool owner = true;
-        for (;;) {   // the run's first position
-            if (a == c0) break;
-            const int64_t pq = sp_prev(q, (int64_t)a);
-            if (pq < 0 || (sp_lookup(q, sp_key(q, (uint64_t)pq, a)) >> 31) == 0u) break;
-            if (sp_bit(q.bits_in, (uint64_t)pq)) { owner = false; break; }   // an earlier seed owns the run
-            a = (uint64_t)pq;
-        }
-        if (!owner) continue;
-        for (uint64_t i = a;;) {   // greedy from the run's first position, which lands
-            const uint64_t j = sp_next(q, i);
-            if (j >= c1) break;
-            const uint32_t v = sp_lookup(q, sp_key(q, i, j));
-            if ((v >> 31) == 0u) break;
-            const uint32_t m = atomicAdd(q.nmerges, 1u);
-            if (m < q.cap) {
-                q.merges[3u * m] = (uint32_t)i;
-                q.merges[3u * m + 1u] = (uint32_t)j;
-                q.merges[3u * m + 2u] = v & 0xFFFFu;
+    const bool from_bits = q.seeds_in == nullptr;
+    const uint32_t ns = from_bits ? (uint32_t)((q.n + 31) / 32) : min(*q.nseeds_in, q.cap);
+    const uint32_t oflag = q.first_pass ? 3u : 1u;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t base = blockIdx.x * 256u + (threadIdx.x & ~63u); base < ns; base += gridDim.x * 256u) {   // (uniform)
+        const uint32_t idx = base + (uint32_t)lane;
+        // this lane's pending seeds: a bitmap word's bits (positions 32 idx + bit), or one list entry
+        uint32_t pend = 0;
+        uint64_t pbase = 0;
+        if (idx < ns) {
+            if (from_bits) {
+                pend = q.bits_in[idx];
+                pbase = 32ull * idx;
             } else {
-                atomicOr(q.flags, 1u);
+                pend = 1u;
+                pbase = q.seeds_in[idx];
             }
-            if ((v >> 30) & 1u) {   // a live token: a seed of the next pass
-                const uint32_t so = atomicAdd(q.nseeds_out, 1u);
+        }
+        bool act = false;
+        uint64_t i = 0, c1 = 0;
+        while (__ballot(act || pend != 0u) != 0ull) {   // (uniform)
+            if (!act && pend != 0u) {   // the next seed: its run's first position, if this lane owns it
+                const uint64_t sd = pbase + (uint64_t)__builtin_ctz(pend);
+                pend &= pend - 1u;
+                if (sd < q.n && !sp_bit(q.holes, sd)) {   // (always: a seed is a token)
+                    // the seed's chunk [c0, c1): the last chunk start <= sd (binary search)
+                    uint64_t lo = 0, hi = q.nchunks;
+                    while (hi - lo > 1) {
+                        const uint64_t mid = (lo + hi) >> 1;
+                        if (q.coff_in[mid] <= sd) lo = mid;
+                        else hi = mid;
+                    }
+                    const uint64_t c0 = q.coff_in[lo];
+                    c1 = lo + 1 < q.nchunks ? q.coff_in[lo + 1] : q.n;
+                    uint64_t a = sd;
+                    bool owner = true;
+                    for (;;) {
+                        if (a == c0) break;
+                        const int64_t pq = sp_prev(q, (int64_t)a);
+                        if (pq < 0 || (sp_lookup(q, sp_key(q, (uint64_t)pq, a)) >> 31) == 0u) break;
+                        if (sp_bit(q.bits_in, (uint64_t)pq)) { owner = false; break; }   // an earlier seed owns the run
+                        a = (uint64_t)pq;
+                    }
+                    act = owner;
+                    i = a;
+                }
+            }
+            // one greedy step from the run's first position, which lands
+            uint64_t j = 0;
+            uint32_t v = 0;
+            if (act) {
+                j = sp_next(q, i);
+                if (j < c1) v = sp_lookup(q, sp_key(q, i, j));
+            }
+            const bool mg = act && (v >> 31) != 0u, lv = mg && ((v >> 30) & 1u);
+            const uint64_t mm = __ballot(mg), lm = __ballot(lv);
+            uint32_t mb = 0, sb = 0;
+            if (lane == 0) {
+                if (mm) mb = atomicAdd(q.nmerges, (uint32_t)__popcll(mm));
+                if (lm) sb = atomicAdd(q.nseeds_out, (uint32_t)__popcll(lm));
+            }
+            mb = (uint32_t)__shfl((int)mb, 0, 64);
+            sb = (uint32_t)__shfl((int)sb, 0, 64);
+            if (mg) {
+                const uint32_t m = mb + (uint32_t)__popcll(mm & below);
+                if (m < q.cap) {
+                    q.merges[3u * m] = (uint32_t)i;
+                    q.merges[3u * m + 1u] = (uint32_t)j;
+                    q.merges[3u * m + 2u] = v & 0xFFFFu;
+                } else {
+                    atomicOr(q.flags, oflag);
+                }
+            }
+            if (lv) {   // a live token: a seed of the next pass
+                const uint32_t so = sb + (uint32_t)__popcll(lm & below);
                 if (so < q.cap) q.seeds_out[so] = (uint32_t)i;
-                else atomicOr(q.flags, 1u);
+                else atomicOr(q.flags, oflag);
                 atomicOr(&q.bits_out[i >> 5], 1u << (i & 31u));
             }
-            const uint64_t k = sp_next(q, j);
-            if (k >= c1) break;
-            // k lands; the run goes on only if (j, k) merges: else k starts the next run, whose own
-            // leftmost seed takes it (k's pair may merge, and two threads would both make it)
-            if ((sp_lookup(q, sp_key(q, j, k)) >> 31) == 0u) break;
-            i = k;
+            if (act) {
+                act = false;
+                if (mg) {
+                    const uint64_t k = sp_next(q, j);
+                    // k lands; the run goes on only if (j, k) merges: else k starts the next run, whose
+                    // own leftmost seed takes it (k's pair may merge, and two lanes would both make it)
+                    if (k < c1 && (sp_lookup(q, sp_key(q, j, k)) >> 31) != 0u) {
+                        i = k;
+                        act = true;
+                    }
+                }
+            }
         }
     }
 }
@@ -3698,7 +3788,7 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
 __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
     if (sp_gated(q)) return;
     const uint32_t nm = *q.flags ? 0u : min(*q.nmerges, q.cap);
-    const uint32_t ns = min(*q.nseeds_in, q.cap);
+    const uint32_t ns = q.seeds_in ? min(*q.nseeds_in, q.cap) : 0u;
     const uint32_t nmax = nm > ns ? nm : ns;
     for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < nmax; idx += gridDim.x * 256u) {
         if (idx < nm) {
@@ -3707,7 +3797,7 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
             atomicOr(&q.holes[j >> 5], 1u << (j & 31u));
             atomicAdd(&q.tile_cnt[j / kSparseTile], 1u);   // holes per compaction tile
         }
-        if (idx < ns) {
+        if (idx < ns) {   // (the first pass's bitmap is not reused)
             const uint32_t sd = q.seeds_in[idx];
             atomicAnd(&q.bits_in[sd >> 5], ~(1u << (sd & 31u)));
         }
@@ -3873,10 +3963,11 @@ __global__ __launch_bounds__(kCpThreads) void sparse_move_kernel(SparseParams qa
         const uint64_t Tn = s_T[it & 1];
         if (tid == 0) {
             if (first) st_publish(q.status + T, 1ull);   // (later tiles were marked when their loads ended)
-            if (ttot != (in_end - tile0) - (hnext - hb)) flag_error(q.ctl, q.sticky, 4u);   // counts vs bitmap
+            if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(q.ctl, q.sticky, 4u);   // counts vs bitmap
         }
         first = false;
-        const bool moves = !(O == tile0 && ttot == in_end - tile0);   // else in place already (uniform)
+        // else in place already; an output range past the tile's input (bad counts) writes nothing
+        const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
         if (moves) {
             if (wave == 0) {   // the earlier tiles whose input the output range overlaps
                 bool bad = false;
@@ -3950,7 +4041,7 @@ __global__ __launch_bounds__(64) void sparse_coff_kernel(SparseParams q, const u
 
 // Host check before any sparse launch: every list and bitmap set, positions in 32 bits.
 static bool sparse_ok(const SparseParams& q) {
-    return q.tok && q.n_dev && q.holes && q.seeds_in && q.nseeds_in && q.bits_in && q.seeds_out && q.nseeds_out &&
+    return q.tok && q.n_dev && q.holes && q.bits_in && q.seeds_out && q.nseeds_out && q.bits_alt &&
            q.bits_out && q.merges && q.nmerges && q.flags && q.cap && q.hbuckets && q.coff_in && q.coff_out &&
            q.tile_cnt && q.super_cnt && q.status && q.ticket && q.n < (1ull << 32);
 }
@@ -3969,10 +4060,27 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
         hipLaunchKernelGGL(sparse_detect_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, q);
     return hipGetLastError();
 }
+hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s) {
+    if (!sparse_ok(q)) return hipErrorInvalidValue;
+    // four rounds of 256 words per workgroup (at most 16384 workgroups: one atomic each)
+    uint64_t g = ((q.n + 31) / 32 + 1023) / 1024;
+    if (g > 16384) g = 16384;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(sparse_list_kernel, dim3((unsigned)g), dim3(256), 0, s, q);
+    return hipGetLastError();
+}
 hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sparse_region_kernel, dim3(256), dim3(256), 0, s, q);
-    hipLaunchKernelGGL(sparse_apply_kernel, dim3(256), dim3(256), 0, s, q);
+    // the first pass: a lane per bitmap word (every word at once: the lanes walk dependent loads);
+    // later passes: lists of a pass's live tokens, mostly short
+    uint64_t rb = 1024;
+    if (!q.seeds_in) {
+        rb = ((q.n + 31) / 32 + 255) / 256;
+        if (rb > 65535) rb = 65535;
+        if (rb < 1) rb = 1;
+    }
+    hipLaunchKernelGGL(sparse_region_kernel, dim3((unsigned)rb), dim3(256), 0, s, q);
+    hipLaunchKernelGGL(sparse_apply_kernel, dim3(q.seeds_in ? 256u : 2048u), dim3(256), 0, s, q);
     return hipGetLastError();
 }
 hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0, hipStream_t s) {

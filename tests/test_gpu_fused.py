@@ -14,6 +14,15 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _fused_before_sparse():
+    """The fused kernel's tests keep it for cyclic maps too: sparse policy 2 (the fused passes, then
+    the sparse ones) instead of the default 4 (the byte pass, then the sparse ones)."""
+    prev = _lib.lib().blt_debug_set_sparse(2)
+    yield
+    _lib.lib().blt_debug_set_sparse(prev)
+
 CHAINED_TEXT_MAP = synth.CHAINED_TEXT_MAP
 
 

@@ -1196,7 +1196,7 @@ def test_sparse_passes(case):
     prev_f = _finish(case != "tail_cut_chunks")
     seen = set()
     try:
-        for policy in (0, 1, 2, 3):
+        for policy in (0, 1, 2, 3, 4):
             _sparse(policy)
             got, lens = s.process_chunks(data, cs, return_chunk_lens=True)
             assert np.array_equal(got, exp), (case, policy)
