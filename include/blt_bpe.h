@@ -152,7 +152,9 @@ int blt_run_tokenizer(const blt_run_config *cfg);
  * Device-resident entry points (inputs already in HBM on the current HIP device).
  * ------------------------------------------------------------------------------------- */
 
-/* Bytes of scratch workspace blt_bpe_encode_device needs for n input bytes. */
+/* Bytes of scratch workspace blt_bpe_encode_device needs for n input bytes.  Depends on the map:
+ * a cyclic general map (a value that can be made from itself, below 2^32 input bytes) adds about
+ * 1.8 n bytes for its sparse passes (bitmaps, seed and merge lists, compaction words). */
 size_t blt_bpe_workspace_size(const blt_bpe *h, uint64_t n, uint64_t chunk_size);
 
 /* Whole-buffer BPE over chunks of chunk_size bytes, on the current device and the given HIP
