@@ -211,3 +211,21 @@ def test_chain_depth_of_general_maps(tmp_path):
     path.write_text(synth.wrap_merges_lines())
     s = blt_amd.BpeStrategy.from_file(str(path))
     assert L.blt_debug_chain_depth(s.handle) == 0           # (255, 255) -> 255
+
+
+def test_workspace_size_of_cyclic_maps():
+    """Host-only: a cyclic general map's workspace holds the sparse passes' bitmaps, lists and
+    compaction words (about 1.75 n bytes more than a bounded map's), below 2^32 input bytes only."""
+    from blt_amd import synth
+    n, cs = 64 << 20, 1 << 20
+    bounded = blt_amd.BpeStrategy(synth.CHAINED_TEXT_MAP)
+    cyclic = blt_amd.BpeStrategy(synth.SELF_VALUED_MAP)
+    single = blt_amd.BpeStrategy({(97, 98): 256})
+    wb, wc, ws = (x.workspace_size(n, cs) for x in (bounded, cyclic, single))
+    assert ws < wb < wc
+    extra = wc - wb
+    assert 1.70 * n < extra < 1.80 * n, extra / n
+    big = 1 << 32   # positions past 32 bits: no sparse passes, no extra workspace
+    assert cyclic.workspace_size(big, cs) == bounded.workspace_size(big, cs)
+    for x in (bounded, cyclic, single):
+        x.close()
