@@ -862,7 +862,8 @@ int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t pass
 //   3 (tests) at the first pass-count read, whatever the last pass merged;
 //   4 (default) enqueued right behind the byte pass (no fused kernel), for maps whose byte pass cannot
 //     end the chain (the others as 3).  On selfval (256 MiB): 0.85 ms against 1.01 with 2 and 1.34
-//     with 0: the byte pass and one sparse first pass (7.6 M merges) cost less than the fused kernel.
+//     with 0: the byte pass and one more sparse pass (u16 pass 1's ~60 K merges) cost less than the
+//     fused kernel.
 // BLT_SPARSE in the environment, or blt_debug_set_sparse, sets it.
 std::atomic<int> g_sparse{getenv("BLT_SPARSE") ? atoi(getenv("BLT_SPARSE")) : 4};
 // Test hook: sparse passes the calling thread's last general-map encode ran (blt_debug_last_sparse):

@@ -3542,8 +3542,8 @@ __device__ __forceinline__ bool sp_compact_skip(const SparseParams& q, const uin
 
 // Every position whose pair with the next one is a merge (not across a chunk start): the first
 // sparse pass's seeds, as a bitmap (bits_in; the first pass reads its seeds from it, so no list and
-// no atomics here: appending millions of seeds to one counter serialised on its address, 561 us on
-// selfval's 8 M).  A lane takes 32 aligned positions (64 bytes of tokens, one word of each bitmap,
+// no atomics here: one append per wave that had seeds serialised on the counter's address, 561 us
+// on selfval's ~60 K seeds).  A lane takes 32 aligned positions (64 bytes of tokens, one word of each bitmap,
 // stored whole: the seed bitmap, the holes and the later passes' two seed bitmaps zeroed); the next
 // lane's first token comes by DPP.  The bucket table is staged in LDS when it fits (kLds).
 template <bool kLds>
@@ -3632,7 +3632,8 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
 // The first pass's seed list from the detect kernel's bitmap: a workgroup per contiguous range of
 // words counts its seeds, reserves its part of the list with one atomic, then writes the seeds in
 // position order, 256 words at a time (a workgroup scan per round).  A first pass that reads its
-// bitmap directly, a lane per word, measured 549 us on selfval's 8 M seeds against 20 us from this list.
+// bitmap directly, a lane per word, measured 549 us on selfval against 20 us from this list (a lane
+// walks its word's seeds one after another, and a long run's seeds sit in few words).
 __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_base, s_run;
@@ -4064,7 +4065,7 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
 }
 hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
-    // 2048 workgroups (one atomic each); 8192 measured 99 us against 40 on selfval's 8 M seeds
+    // 2048 workgroups (one atomic each); 8192 measured 99 us against 40 on selfval
     uint64_t g = ((q.n + 31) / 32 + 255) / 256;
     if (g > 2048) g = 2048;
     if (g < 1) g = 1;
