@@ -162,7 +162,7 @@ def extra_configs(blt_amd, synth, O, threads, only=()):
                      "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
         del d_in, d_out, got, exp, host
         s.close()
-    for name in ("multi", "wrap", "selfval", "chain"):
+    for name in ("multi", "wrap", "selfval", "chain", "cyclic_dense"):
         if only and name not in only:
             continue
         res[name] = general_map_rate(blt_amd, synth, O, threads, name)
@@ -211,6 +211,15 @@ def general_workload(synth, name):
         m = synth.SELF_VALUED_MAP
         return synth.text(256 << 20, seed=2), lambda: blt_amd.BpeStrategy(m), m, \
             "f2: 256 MiB synthetic text, 4 merges two of which are valued their own first byte (generic byte pass)"
+    if name == "cyclic_dense":
+        # a cyclic map whose byte pass leaves a mergeable pair at every word start: (' ', c) -> ' '
+        # eats one letter after each space per pass; the key (300, 301) (never made) keeps it off the
+        # byte-pair-key path, so its sparse passes are tried right behind the byte pass and not taken
+        # (the detect gate)
+        m = {(32, c): 32 for c in range(97, 123)}
+        m[(300, 301)] = 302
+        return synth.text(256 << 20, seed=2), lambda: blt_amd.BpeStrategy(m), m, \
+            "f2: 256 MiB synthetic text, a cyclic map ((' ', letter) -> ' ') whose passes merge densely"
     if name == "chain":
         m = synth.doubling_chain(24)
         return np.full(256 << 20, 97, np.uint8), lambda: blt_amd.BpeStrategy(m), m, \

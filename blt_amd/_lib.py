@@ -98,7 +98,6 @@ _DEBUG_SIGNATURES = {
     "blt_debug_byte_mode": (ctypes.c_int, [_vp]),
     "blt_debug_chain_depth": (ctypes.c_uint32, [_vp]),
     "blt_debug_set_finish": (ctypes.c_int, [ctypes.c_int]),
-    "blt_debug_set_chain": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_set_sparse": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_last_sparse": (ctypes.c_uint32, []),
     "blt_debug_set_sparse_cap": (ctypes.c_uint32, [ctypes.c_uint32]),

@@ -191,6 +191,7 @@ static double since_exec() {
 }
 
 int main(int argc, char** argv) {
+    blt_log_init_from_env();   // tracing_subscriber::fmt().with_env_filter(RUST_LOG) (main.rs:83-85)
     const double t_main = mono_now();
     const double t_exec = getenv("BLT_CLI_TIMING") ? since_exec() : 0.0;
     const Args a = parse_args(argc, argv);

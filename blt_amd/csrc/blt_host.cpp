@@ -281,6 +281,10 @@ struct blt_bpe {
     // that checks it before its own first sticky_word() never races the allocating thread.
     std::once_flag sticky_once;
     std::atomic<uint32_t*> sticky{nullptr};
+    // Pinned host words of the sparse passes' reads (SparseHost), one per concurrent encode: taken
+    // from this free list and returned after the run, freed by blt_bpe_destroy.
+    mutable std::mutex sp_mu;
+    mutable std::vector<void*> sp_free;
 };
 
 namespace {
@@ -577,7 +581,7 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
-    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, stat2, pctr, bytes, zero_bytes;
+    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, bytes, zero_bytes;
     // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
     // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
     uint64_t sp_holes, sp_bits0, sp_bits1, sp_bits2, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles;
@@ -590,7 +594,7 @@ inline bool chain_bounded(const blt_bpe* h) { return h->chain_depth && h->chain_
 // the full passes).  Counter words: [0] overflow flag, [1] compaction ticket, [2 + p] pass p's seeds,
 // [2 + kSparseMaxPasses + 1 + p] pass p's merges.
 constexpr uint32_t kSparseMaxPasses = 250;
-constexpr uint32_t kSparseCtrWords = 2 + 2 * (kSparseMaxPasses + 1);
+constexpr uint32_t kSparseCtrWords = 2 + 2 * (kSparseMaxPasses + 1) + 1;   // + the detect gate's sample count
 // Chain block of a general map (right after pass 1's status words): u64 pass totals [2], u32 done
 // word, u32 fused-fail word, u64 final total, u32 finish-gate word, pad.
 constexpr uint64_t kChainBlock = 48;
@@ -615,9 +619,7 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
     L.gstat = L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));   // finish: a status word per group
-    L.stat2 = L.gstat + up16(8 * L.nchunks);   // chain launches: the second status area, per token tile
-    L.pctr = L.stat2 + up16(8 * L.ntiles);     // chain launches: ticket and emitted counters per pass
-    L.bytes = single_pass ? L.cmap : L.pctr + 8ull * blt::kChainMaxPasses;
+    L.bytes = single_pass ? L.cmap : L.gstat + up16(8 * L.nchunks);
     if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
         const uint64_t bm = up16(4 * ((n + 31) / 32));
         const uint64_t cap = n / 16 + 4096;
@@ -728,49 +730,6 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     return 0;
 }
 
-// u16 passes k .. k + np - 1 of a general map in one launch (blt::launch_scan_chain), as np
-// run_pass calls on the scan kernel would run them: tokens in place in d_out, chunk starts from
-// off_in (then the arrays alternate), totals tot[k & 1], tot[(k + 1) & 1], ...
-int run_chain(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
-              uint8_t* d_out, uint64_t n, uint32_t k, uint32_t np, const uint64_t* off_in, uint64_t* off_out,
-              uint64_t* tot, uint32_t* done) {
-    blt::PassParams p{};
-    p.in = d_out;
-    p.n = n;
-    p.cstart = off_in;
-    p.nchunks = L.nchunks;
-    p.out = d_out;
-    p.out_cap = 2 * n;
-    p.chunk_off = off_out;
-    p.status = reinterpret_cast<uint64_t*>(ws + L.status);
-    p.status2 = reinterpret_cast<uint64_t*>(ws + L.stat2);
-    p.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
-    p.pass_ctr = reinterpret_cast<uint32_t*>(ws + L.pctr);
-    p.npasses = np;
-    p.n_dev = tot + ((k - 1) & 1);
-    p.total = tot + (k & 1);
-    p.done = done;
-    p.pass_id = k;
-    p.ntiles = (uint32_t)((n + blt::kTilePosTok - 1) / blt::kTilePosTok);
-    p.hbuckets = t->hbuckets;
-    p.hmul1 = h->hmul1;
-    p.hmul2 = h->hmul2;
-    p.hshift = h->hshift;
-    p.hbytes = (uint32_t)(h->hwords.size() * sizeof(uint32_t));
-    p.hone = h->hone ? 1u : 0u;
-    p.sticky = h->sticky.load(std::memory_order_acquire);
-    p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
-    HIP_TRY(blt::launch_scan_chain(p, dev, s));
-    return 0;
-}
-
-// Chain launches are off by default: measured, one persistent launch of a chain's passes costs
-// what the separate launches do (f2 chain 0.666 ms either way, selfval 1.34 -> 1.39 ms with them;
-// profiles/r04_chain_ab.txt): a pass's barrier drains and refills every workgroup's pipeline as a
-// kernel boundary does, and the launch loses the nt cache policy to the sc1 hand-off.  Test hook
-// blt_debug_set_chain(1), or BLT_CHAIN=1 in the environment, turns them on.
-std::atomic<int> g_chain{getenv("BLT_CHAIN") && getenv("BLT_CHAIN")[0] == '1' ? 1 : 0};
-
 // Passes 1 and 2 of a general map in one launch (blt::launch_scan_fused): bytes d_in to the second
 // pass's tokens in d_out, its total, chunk offsets and done word as u16 pass 1's.
 int run_fused(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
@@ -855,17 +814,13 @@ int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t pass
 }
 
 // Sparse passes of a cyclic map (blt::launch_sparse_*; bpe_kernels.hip explains why they are the
-// greedy passes), tried once per encode:
-//   0 off;
-//   1 at the first pass-count read whose last pass merged under 1/16 of its tokens;
-//   2 enqueued right behind the fused passes 1 + 2, then as 3;
-//   3 (tests) at the first pass-count read, whatever the last pass merged;
-//   4 (default) enqueued right behind the byte pass (no fused kernel), for maps whose byte pass cannot
-//     end the chain (the others as 3).  On selfval (256 MiB): 0.85 ms against 1.01 with 2 and 1.34
-//     with 0: the byte pass and one more sparse pass (u16 pass 1's ~60 K merges) cost less than the
-//     fused kernel.
-// BLT_SPARSE in the environment, or blt_debug_set_sparse, sets it.
-std::atomic<int> g_sparse{getenv("BLT_SPARSE") ? atoi(getenv("BLT_SPARSE")) : 4};
+// greedy passes), tried once per encode: enqueued right behind the byte pass (no fused kernel) for
+// maps whose byte pass cannot end the chain, at the first read of the pass counts for the others.
+// On selfval (256 MiB): 0.85 ms against 1.01 behind the fused passes 1 + 2 and 1.34 with full
+// passes only: the byte pass and one more sparse pass (u16 pass 1's ~60 K merges) cost less than
+// the fused kernel.  Test hook blt_debug_set_sparse(0) turns them off (full passes only, the fused
+// kernel where it applies).
+std::atomic<int> g_sparse{1};
 // Test hook: sparse passes the calling thread's last general-map encode ran (blt_debug_last_sparse):
 // passes | 1 << 16 when they reached the fixpoint, | 1 << 17 when a list overflowed.
 thread_local uint32_t t_last_sparse = 0;
@@ -877,21 +832,39 @@ struct SparseRun {
     bool gated = false;      // the chain had ended (or the fused kernel must fall back): nothing ran
     bool taken = false;      // detect found few enough seeds: the passes ran
     bool complete = false;   // ... to the fixpoint (else the full passes go on from the compaction)
-    uint32_t passes = 0;     // passes enqueued (an upper bound of those that merged)
+    uint32_t passes = 0;     // passes enqueued: the compaction wrote the total as pass k + passes - 1's
+    uint32_t applied = 0;    // passes that did work: up to the last with seeds, before any overflow
     uint64_t rec[4] = {0, 0, 0, 0};   // the chain block's totals, done and fallback words, as read last
     bool rec_final = false;  // ... read after the compaction
 };
 
-// Host words of the sparse passes' reads (pinned: the reads sit between the device's launches).
+// Host words of the sparse passes' reads (pinned: the reads sit between the device's launches),
+// from the handle's free list (blt_bpe::sp_free); a failed allocation leaves the sparse passes out
+// of that encode (the full passes give the same tokens).
 struct SparseHost {
     uint32_t ctr[kSparseCtrWords];
     uint64_t rec[4];
 };
-SparseHost* sparse_host() {
-    thread_local SparseHost* p = nullptr;
-    if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(SparseHost), hipHostMallocDefault) != hipSuccess) p = nullptr;
-    return p;
-}
+struct SparseHostLease {
+    const blt_bpe* h;
+    SparseHost* p = nullptr;
+    explicit SparseHostLease(const blt_bpe* hh) : h(hh) {
+        {
+            std::lock_guard<std::mutex> lk(h->sp_mu);
+            if (!h->sp_free.empty()) {
+                p = static_cast<SparseHost*>(h->sp_free.back());
+                h->sp_free.pop_back();
+            }
+        }
+        if (!p && hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(SparseHost), hipHostMallocDefault) != hipSuccess)
+            p = nullptr;
+    }
+    ~SparseHostLease() {
+        if (!p) return;
+        std::lock_guard<std::mutex> lk(h->sp_mu);
+        h->sp_free.push_back(p);
+    }
+};
 
 // After u16 pass k - 1 (its token count at n_dev on the device, at most n_max, in place in d_out;
 // chunk starts off_in): sparse passes k, k + 1, ... in the hole layout, then the compaction into
@@ -905,7 +878,8 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
                uint8_t* d_out, const uint64_t* n_dev, uint64_t n_max, const uint64_t* gate, uint64_t k,
                const uint64_t* off_in, uint64_t* off_out, uint64_t* tot, SparseRun* r) {
     *r = SparseRun{};
-    SparseHost* hb = sparse_host();
+    SparseHostLease lease(h);
+    SparseHost* hb = lease.p;
     if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
     (void)dev;
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
@@ -933,6 +907,7 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.super_cnt = q.tile_cnt + ((L.sp_ntiles + 15) & ~15ull);
     q.status = reinterpret_cast<uint64_t*>(ws + L.sp_status);
     q.ticket = ctr + 1;
+    q.sample = ctr + (kSparseCtrWords - 1);
     q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     q.sticky = h->sticky.load(std::memory_order_acquire);
     uint32_t* seeds[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_seeds0), reinterpret_cast<uint32_t*>(ws + L.sp_seeds1)};
@@ -970,7 +945,19 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.total = tot + ((k + kFirst - 1) & 1);
     HIP_TRY(blt::launch_sparse_compact(q, nseeds0, s));
     uint32_t* c = hb->ctr;
-    HIP_TRY(hipMemcpyAsync(c, ctr, 4ull * (2 + kFirst + 1), hipMemcpyDeviceToHost, s));
+    // passes that did work, of the pp enqueued: those before the first that overflowed a list (its
+    // merges were dropped and every later region kernel returned at once), and of those the ones up
+    // to the last that had seeds (a pass without seeds merges nothing)
+    auto applied = [&](uint32_t npass) {
+        uint32_t a = 0;
+        for (uint32_t p = 0; p < npass; ++p) {
+            if (c[2 + (kSparseMaxPasses + 1) + p] > q.cap || c[2 + p + 1] > q.cap) break;
+            if (c[2 + p] == 0) break;
+            a = p + 1;
+        }
+        return a;
+    };
+    HIP_TRY(hipMemcpyAsync(c, ctr, sizeof hb->ctr, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(hb->rec, tot, 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::copy(hb->rec, hb->rec + 4, r->rec);
@@ -984,6 +971,7 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     if (c[2 + kFirst] == 0) {   // the compaction ran
         r->rec_final = true;
         r->passes = kFirst;
+        r->applied = applied(kFirst);
         r->complete = !overflow;
         t_last_sparse = kFirst | (r->complete ? 1u << 16 : 0u) | (overflow ? 1u << 17 : 0u);
         return 0;
@@ -994,11 +982,12 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
             at_pass(pp);
             HIP_TRY(blt::launch_sparse_pass(q, s));
         }
-        HIP_TRY(hipMemcpyAsync(c, ctr, 4ull * (2 + pp + 1), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c, ctr, sizeof hb->ctr, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         overflow = c[0] != 0;
     }
     r->passes = pp;
+    r->applied = applied(pp);
     r->complete = !overflow && c[2 + pp] == 0;
     q.cond = nullptr;
     q.total = tot + ((k + pp - 1) & 1);
@@ -1063,10 +1052,11 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
     // keep the byte pass, which can); its halo fallback is read where the host reads the chain's
     // totals anyway, so an async bounded chain keeps the two-kernel path.
-    const int sp_policy = L.sp_cap ? g_sparse.load(std::memory_order_relaxed) : 0;
+    // (a cyclic map whose byte pass cannot end the chain takes the sparse passes right behind the
+    // byte pass instead: see g_sparse)
+    const bool sp_on = L.sp_cap && g_sparse.load(std::memory_order_relaxed) != 0;
     const bool fused = !(flags & kEncodeNoFused) && g_fused.load(std::memory_order_relaxed) && !h->live_first &&
-                       !(sp_policy == 4 && !h->live_first) &&
-                       !h->byte_self_pair &&
+                       !sp_on && !h->byte_self_pair &&
                        h->hwords.size() * sizeof(uint32_t) <= blt::kHashLdsMax && cs >= blt::kMinChunkBytes &&
                        (!bounded || out_tokens != nullptr);
     uint32_t* fused_fail = reinterpret_cast<uint32_t*>(ws + L.total + 20);   // beside the done word
@@ -1110,19 +1100,6 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         fin_tried = true;
         return true;
     };
-    // passes from k on that one chain launch can run (at most lim): scan-kernel passes (every chunk
-    // at least kTokRange tokens), none of them the finish kernels' pass; 0 or 1: separate launches
-    const bool chain_ok = g_chain.load(std::memory_order_relaxed) && L.nchunks <= blt::kChainMaxChunks &&
-                          n < (1ull << 31);   // (token positions in 32 bits in the chain kernel)
-    auto chain_len = [&](uint64_t k0, uint64_t lim) {
-        uint64_t np = 0;
-        if (!chain_ok) return np;
-        for (uint64_t kk = k0; np < lim && np < blt::kChainMaxPasses; ++kk, ++np) {
-            if (kk >= 64 || (cs >> kk) < blt::kTokRange) break;
-            if (!fin_tried && (cs >> kk) <= blt::kFinCapTokens) break;
-        }
-        return np;
-    };
     if (bounded) {
         // a bounded chain (no value can be made from itself): u16 passes 1 .. depth - 1 are all a
         // pass can need, enqueued without reading the device's pass count; passes after the one
@@ -1130,14 +1107,6 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         // and chunk offsets.  Only a caller asking for the token count waits (once).
         const uint32_t k_last = h->chain_depth - 1;
         for (; k <= k_last; ++k) {
-            if (const uint64_t np = chain_len(k, k_last - k + 1); np >= 2) {
-                if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
-                                       tot, done))
-                    return rc;
-                cur ^= (int)(np & 1);
-                k += np - 1;
-                continue;
-            }
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
@@ -1169,31 +1138,40 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         *out_tokens = rec[3];
         return 0;
     }
-    // sparse passes: tried once (policy 2: right after the fused passes, enqueued behind them;
-    // policy 4: right after the byte pass)
-    bool sp_tried = sp_policy == 0;
+    // sparse passes: tried once, right behind the byte pass or at the first read of the pass counts
+    bool sp_tried = !sp_on;
     t_last_sparse = 0;
+    // Before pass k the chain's arrays follow k: its input total is tot[(k - 1) & 1] and it writes
+    // tot[k & 1].  The chunk offsets follow cur, which a sparse run flips once whatever number of
+    // passes it ran: pass k reads off[cur] = off[((k - 1) & 1) ^ off_shift] and writes the other.
+    uint32_t off_shift = 0;
+    // passes enqueued that did nothing (a sparse run's passes after its fixpoint or its overflow):
+    // k counts them (the compaction wrote its total as the last enqueued pass's), the pass counts
+    // reported and checked do not
+    uint64_t k_idle = 0;
     // a sparse run that was taken: the passes it ran, then the compaction's results, or the end
     auto sparse_taken = [&](const SparseRun& r, bool* finished) -> int {
         *finished = false;
         cur ^= 1;
         k += r.passes;
+        k_idle += r.passes - r.applied;
+        off_shift = (uint32_t)cur ^ (uint32_t)((k - 1) & 1);
         if (!r.rec_final) {   // (the totals to read)
             HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
             HIP_TRY(hipStreamSynchronize(s));
         } else {
             std::copy(r.rec, r.rec + 4, rec);
         }
-        if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
+        if (int rc = chain_sticky(h, ws, L, k - 1 - k_idle)) return rc;
         if (!r.complete) return 0;
         *finished = true;
-        t_last_u16_passes = (uint32_t)(k - 1);
+        t_last_u16_passes = (uint32_t)(k - 1 - k_idle);
         if (d_chunk_off && off[cur] != d_chunk_off)
             HIP_TRY(hipMemcpyAsync(d_chunk_off, off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
         if (out_tokens) *out_tokens = rec[(k - 1) & 1];
         return 0;
     };
-    if ((sp_policy == 2 && fused) || (sp_policy == 4 && !fused && !bounded && !h->live_first)) {
+    if (sp_on && !bounded && !h->live_first) {   // (no fused kernel: see fused above)
         sp_tried = true;
         SparseRun r;
         const uint64_t* gate = reinterpret_cast<const uint64_t*>(done);   // done word | fallback word
@@ -1208,15 +1186,6 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     }
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
-            if (const uint64_t np = chain_len(k, (uint64_t)(batch - b)); np >= 2) {
-                if (int rc = run_chain(h, t, dev, s, ws, L, d_out, n, (uint32_t)k, (uint32_t)np, off[cur], off[cur ^ 1],
-                                       tot, done))
-                    return rc;
-                cur ^= (int)(np & 1);
-                k += np - 1;
-                b += (int)np - 1;
-                continue;
-            }
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
             if (finish_now(k))
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
@@ -1229,13 +1198,13 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         }
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (int rc = chain_sticky(h, ws, L, k - 1)) return rc;
+        if (int rc = chain_sticky(h, ws, L, k - 1 - k_idle)) return rc;
         if (fused && (rec[2] >> 32)) return fallback();
         if ((uint32_t)rec[2]) break;
-        if (k > n + 8) return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)k);
-        // the last pass k - 1 left N tokens out of Nin (Nin unknown after the fused passes)
-        const uint64_t N = rec[(k - 1) & 1], Nin = (k >= 3 || !fused) ? rec[k & 1] : 0;
-        if (!sp_tried && (sp_policy >= 2 || (Nin >= N && (Nin - N) * 16 < N))) {
+        if (k - k_idle > n + 8)
+            return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)(k - k_idle));
+        const uint64_t N = rec[(k - 1) & 1];   // the tokens the last pass left
+        if (!sp_tried) {
             sp_tried = true;
             SparseRun r;
             if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), N, nullptr, k, off[cur],
@@ -1249,10 +1218,12 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         }
     }
     const uint32_t kdone = (uint32_t)rec[2] & ~blt::kDoneBytePass;   // 0: pass 1 was final
-    t_last_u16_passes = kdone;
-    const uint32_t last = kdone & 1u;   // the arrays the final pass wrote
-    if (d_chunk_off && off[last] != d_chunk_off)
-        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[last], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
+    t_last_u16_passes = (uint32_t)(kdone ? kdone - k_idle : 0);
+    const uint32_t last = kdone & 1u;              // the total the final pass wrote
+    const uint32_t olast = last ^ off_shift;       // and its chunk offsets (not off[last]
+                                                   // after a sparse run of an even number of passes)
+    if (d_chunk_off && off[olast] != d_chunk_off)
+        HIP_TRY(hipMemcpyAsync(d_chunk_off, off[olast], 8 * (L.nchunks + 1), hipMemcpyDeviceToDevice, s));
     if (out_tokens) *out_tokens = rec[last];
     return 0;
 }
@@ -1770,6 +1741,7 @@ void blt_bpe_destroy(blt_bpe* h) {
         if (h->dev[d].hbuckets) (void)hipFree(h->dev[d].hbuckets);
     }
     if (uint32_t* w = h->sticky.load(std::memory_order_acquire)) (void)hipHostFree(w);
+    for (void* p : h->sp_free) (void)hipHostFree(p);
     delete h;
 }
 
@@ -1840,8 +1812,7 @@ int blt_debug_byte_mode(const blt_bpe* h) {
 // Not in the public header (tests): 0 disables the finish kernels of a general map's chain, 1 (the
 // default) enables them; returns the previous setting.
 int blt_debug_set_finish(int on) { return g_finish.exchange(on ? 1 : 0); }
-int blt_debug_set_chain(int on) { return g_chain.exchange(on ? 1 : 0); }
-int blt_debug_set_sparse(int policy) { return g_sparse.exchange(policy); }
+int blt_debug_set_sparse(int on) { return g_sparse.exchange(on ? 1 : 0); }
 uint32_t blt_debug_last_sparse(void) { return t_last_sparse; }
 uint32_t blt_debug_set_sparse_cap(uint32_t cap) { return g_sparse_cap.exchange(cap); }
 

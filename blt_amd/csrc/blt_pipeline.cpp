@@ -28,6 +28,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -37,6 +38,9 @@
 #include <thread>
 #include <vector>
 
+#include <stdarg.h>
+#include <strings.h>
+
 #include "../../include/blt_bpe.h"
 
 namespace blt_internal {
@@ -44,9 +48,109 @@ int set_error(int code, const char* fmt, ...);
 }
 using blt_internal::set_error;
 
+// ---- logging (the reference's tracing, src/main.rs:83-85) ----------------------------------
+// blt_log_init_from_env sets the level from RUST_LOG (BLT_LOG when unset): a comma list of
+// directives, each "level", "target" or "target=level"; the most verbose level among the directives
+// whose target is a prefix of blt_core's (or that name none) applies; none applicable: errors only
+// (EnvFilter's default).  Before the call (library users other than the CLI, as the Python binding)
+// nothing is logged.  Lines go to stdout with one write(2) each (tracing's fmt subscriber writes to
+// stdout; the run's own stdout writes are unbuffered too, so the order is the order of the calls).
+namespace blt_log {
+enum Level { kOff = 0, kError, kWarn, kInfo, kDebug, kTrace };
+std::atomic<int> g_level{-1};   // -1: not initialised (nothing is logged)
+std::mutex g_mu;
+
+int parse_level(const char* s, size_t n) {
+    static const char* names[] = {"off", "error", "warn", "info", "debug", "trace"};
+    for (int i = 0; i < 6; ++i)
+        if (strlen(names[i]) == n && strncasecmp(s, names[i], n) == 0) return i;
+    return -1;
+}
+
+int level_from(const char* v) {
+    int best = -1;
+    for (const char* d = v; d && *d;) {
+        const char* e = strchr(d, ',');
+        const size_t n = e ? (size_t)(e - d) : strlen(d);
+        std::string dir(d, n);
+        while (!dir.empty() && dir.back() == ' ') dir.pop_back();
+        while (!dir.empty() && dir.front() == ' ') dir.erase(dir.begin());
+        const size_t eq = dir.find('=');
+        int lv = -1;
+        if (eq == std::string::npos) {
+            lv = parse_level(dir.data(), dir.size());
+            if (lv < 0 && !dir.empty() && std::string("blt_core::pipeline").compare(0, dir.size(), dir) == 0)
+                lv = kTrace;   // a bare target enables every level of it
+        } else {
+            const std::string target = dir.substr(0, eq);
+            if (std::string("blt_core::pipeline").compare(0, target.size(), target) == 0 ||
+                std::string("blt_core::tokenizer").compare(0, target.size(), target) == 0)
+                lv = parse_level(dir.data() + eq + 1, dir.size() - eq - 1);
+        }
+        if (lv > best) best = lv;
+        d = e ? e + 1 : nullptr;
+    }
+    return best < 0 ? (int)kError : best;
+}
+
+bool on(int lv) { return g_level.load(std::memory_order_relaxed) >= lv; }
+
+// "<UTC time>  LEVEL <spans>: <target>: <message>"
+void emit(int lv, const char* spans, const char* target, const char* fmt, ...) {
+    if (!on(lv)) return;
+    static const char* names[] = {"", "ERROR", " WARN", " INFO", "DEBUG", "TRACE"};
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    struct tm tm;
+    gmtime_r(&ts.tv_sec, &tm);
+    char line[1024];
+    int k = snprintf(line, sizeof line, "%04d-%02d-%02dT%02d:%02d:%02d.%06ldZ %s %s%s%s: ", tm.tm_year + 1900,
+                     tm.tm_mon + 1, tm.tm_mday, tm.tm_hour, tm.tm_min, tm.tm_sec, ts.tv_nsec / 1000, names[lv],
+                     spans ? spans : "", spans && *spans ? ": " : "", target);
+    va_list ap;
+    va_start(ap, fmt);
+    if (k > 0 && (size_t)k < sizeof line) k += vsnprintf(line + k, sizeof line - (size_t)k, fmt, ap);
+    va_end(ap);
+    if (k < 0) return;
+    if ((size_t)k >= sizeof line - 1) k = (int)sizeof line - 2;
+    line[k++] = '\n';
+    std::lock_guard<std::mutex> g(g_mu);
+    for (const char* p = line; k > 0;) {
+        const ssize_t w = ::write(1, p, (size_t)k);
+        if (w <= 0) {
+            if (w < 0 && errno == EINTR) continue;
+            return;
+        }
+        p += w;
+        k -= (int)w;
+    }
+}
+}  // namespace blt_log
+
+extern "C" void blt_log_init_from_env(void) {
+    const char* v = getenv("RUST_LOG");
+    if (!v) v = getenv("BLT_LOG");
+    blt_log::g_level.store(blt_log::level_from(v), std::memory_order_relaxed);
+}
+
 namespace {
 
 constexpr size_t kStdinReadCap = size_t(2) << 20;   // tokio io::blocking DEFAULT_MAX_BUF_SIZE
+
+// Debug lines of the chunks [k0, k1) of a file input (pipeline.rs:108 per received result; the
+// basic strategy's per-chunk line, tokenizer.rs:113).
+void log_chunks(const std::string& span, bool basic, size_t k0, size_t k1, size_t n, size_t cs) {
+    if (!blt_log::on(blt_log::kDebug)) return;
+    for (size_t k = k0; k < k1; ++k) {
+        if (basic) {
+            const std::string sp = span + ":process_mmap_chunk_task{task_id=" + std::to_string(k) +
+                                   "}:basic_tokenization_strategy_process";
+            blt_log::emit(blt_log::kDebug, sp.c_str(), "blt_core::tokenizer", "Converting %zu bytes to u16 tokens",
+                          std::min(cs, n - k * cs));
+        }
+        blt_log::emit(blt_log::kDebug, span.c_str(), "blt_core::pipeline", "Received result for mmap task task_id=%zu", k);
+    }
+}
 
 // First error of a run wins; later ones are dropped.
 struct RunStatus {
@@ -177,7 +281,7 @@ struct Strategy {
 
 // mmap path (pipeline.rs:56-192): windows of whole chunks, window k+1 tokenised while window k is
 // written.
-int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& sink) {
+int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& sink, const std::string& span) {
     if (n == 0) return 0;
     const size_t per = std::max<size_t>(1, (size_t(256) << 20) / cs);   // ~256 MiB of input per window
     const size_t win = per * cs;
@@ -208,6 +312,7 @@ int run_mmap(const Strategy& st, const uint8_t* in, size_t n, size_t cs, Sink& s
         }
         if (wrc) break;
         if (rc) break;
+        log_chunks(span, st.kind == Strategy::kBasic, off / cs, (off + len + cs - 1) / cs, n, cs);
         writer = std::thread([&sink, &out, &wrc, &wmsg] {
             wrc = sink.write_all(out.p.get(), out.len);
             if (wrc) wmsg = last_error();
@@ -250,7 +355,7 @@ struct OutMap {
 void map_output(int fd, size_t total, size_t est, OutMap* om);
 
 int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, int fd, size_t head,
-                    const uint8_t* head_bytes, const OutMap& om) {
+                    const uint8_t* head_bytes, const OutMap& om, const std::string& span) {
     const size_t cap = st.kind == Strategy::kPassthrough ? n : 2 * n;
     const size_t total = head + cap;
     if (total == 0) return 0;
@@ -279,6 +384,7 @@ int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, 
             olen += w;
         }
     }
+    if (!rc) log_chunks(span, st.kind == Strategy::kBasic, 0, (n + cs - 1) / cs, n, cs);
     if (om.registered) (void)hipHostUnregister(om.m);
     munmap(om.m, total);
     const std::string msg = rc ? last_error() : std::string();
@@ -347,7 +453,9 @@ void map_output(int fd, size_t total, size_t est, OutMap* om) {
 // Stream path (pipeline.rs:196-433): one read per chunk, at most `threads` chunks in flight, a
 // worker pool tokenises (each call stages its chunk through the GPU; the handle is reentrant), a
 // writer emits results in chunk order.  Any error stops reading and is returned.
-int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& sink) {
+int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& sink, const std::string& span) {
+    const bool dbg = blt_log::on(blt_log::kDebug);
+    const std::string sp_read = span + ":manage_task_spawning";
     threads = std::max<size_t>(1, threads);
     const size_t nworkers = std::min<size_t>(threads, 16);
     const size_t rd = std::min(cs, kStdinReadCap);
@@ -373,9 +481,21 @@ int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& s
                     jobs.pop_front();
                 }
                 std::vector<uint8_t> out;
+                if (dbg && st.kind == Strategy::kBasic && !job.second.empty()) {
+                    const std::string sp = span + ":process_chunk_task{task_id=" + std::to_string(job.first) +
+                                           "}:basic_tokenization_strategy_process";
+                    blt_log::emit(blt_log::kDebug, sp.c_str(), "blt_core::tokenizer", "Converting %zu bytes to u16 tokens",
+                                  job.second.size());
+                }
                 const int rc = st.chunk(job.second.data(), job.second.size(), out);
                 std::lock_guard<std::mutex> lk(mu);
+                if (dbg) blt_log::emit(blt_log::kDebug, span.c_str(), "blt_core::pipeline", "Received result for task task_id=%llu",
+                                       (unsigned long long)job.first);
                 if (rc) {
+                    // (pipeline.rs:409: the error reaches the ordered writer; here the first error stops the run)
+                    blt_log::emit(blt_log::kError, span.c_str(), "blt_core::pipeline",
+                                  "Error in processed chunk: %s chunk_id=%llu", last_error().c_str(),
+                                  (unsigned long long)job.first);
                     status.set(rc, last_error());
                     stop = true;
                 } else {
@@ -394,6 +514,8 @@ int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& s
             std::vector<uint8_t> out = std::move(it->second);
             results.erase(it);
             lk.unlock();
+            if (dbg) blt_log::emit(blt_log::kDebug, span.c_str(), "blt_core::pipeline", "Writing ordered chunk to output chunk_id=%llu bytes=%zu",
+                                   (unsigned long long)n_written, out.size());
             const int rc = sink.write_all(out.data(), out.size());
             const std::string m = rc ? last_error() : std::string();
             lk.lock();
@@ -428,11 +550,14 @@ int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& s
             break;
         }
         if (r == 0) {
+            if (dbg) blt_log::emit(blt_log::kDebug, sp_read.c_str(), "blt_core::pipeline", "Input stream reached EOF");
             eof = true;
             cv.notify_all();
             break;
         }
         chunk.resize((size_t)r);
+        if (dbg) blt_log::emit(blt_log::kDebug, sp_read.c_str(), "blt_core::pipeline", "Spawning chunk processing task task_id=%llu bytes=%zd",
+                               (unsigned long long)n_read, r);
         jobs.emplace_back(n_read++, std::move(chunk));
         ++in_flight;
         cv.notify_all();
@@ -459,10 +584,21 @@ int run(const blt_run_config* c) {
     if (!c) return set_error(BLT_E_INVALID_INPUT, "null config");
     if (c->chunk_size == 0) return set_error(BLT_E_INVALID_INPUT, "chunk_size must be > 0");
     if (c->content_token > 0xFFFFu) return set_error(BLT_E_INVALID_INPUT, "content token 0x%x is not a u16", c->content_token);
+    // the run_tokenizer span (lib.rs:245: fields input, output as Option<PathBuf> Debug)
+    auto opt = [](const char* path) { return path ? "Some(\"" + std::string(path) + "\")" : std::string("None"); };
+    const std::string span = "run_tokenizer{input=" + opt(c->input_path) + " output=" + opt(c->output_path) + "}";
+    const std::string span_pipe = span + ":run_pipeline";
+    blt_log::emit(blt_log::kInfo, span.c_str(), "blt_core", "Starting tokenizer");
     Strategy st;
     if (c->passthrough) st.kind = Strategy::kPassthrough;   // lib.rs:272-274: passthrough wins
     else if (c->bpe) st.kind = Strategy::kBpe;
     else st.kind = Strategy::kBasic;
+    blt_log::emit(blt_log::kInfo, span.c_str(), "blt_core",
+                  st.kind == Strategy::kPassthrough ? "Using passthrough strategy (file copying without tokenization)."
+                  : st.kind == Strategy::kBpe      ? "Using BPE tokenization strategy."
+                                                    : "Using basic tokenization strategy (byte-to-u16 conversion).");
+    blt_log::emit(blt_log::kInfo, span.c_str(), "blt_core", "Chunk size determined effective_chunk_size=%llu",
+                  (unsigned long long)c->chunk_size);
     st.h = c->bpe;
     st.gpus = c->n_gpus;
     const size_t cs = (size_t)c->chunk_size;
@@ -606,15 +742,19 @@ int run(const blt_run_config* c) {
 
     int rc = 0;
     const uint8_t tok[2] = {(uint8_t)(c->content_token >> 8), (uint8_t)c->content_token};
+    if (c->input_path)
+        blt_log::emit(blt_log::kInfo, span_pipe.c_str(), "blt_core::pipeline", "Running pipeline in Mmap mode for file of size: %zu", n);
+    else
+        blt_log::emit(blt_log::kInfo, span_pipe.c_str(), "blt_core::pipeline", "Running pipeline in Stream mode for stdin");
     int drc = 1;
-    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om);
+    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om, span_pipe);
     if (drc <= 0) {
         rc = drc;
     } else {
         if (c->content_token) rc = sink.write_all(tok, 2);   // prepend_content_type_token (lib.rs:284-293)
         if (!rc) {
-            if (c->input_path) rc = run_mmap(st, map, n, cs, sink);
-            else rc = run_stream(st, 0, cs, (size_t)c->threads, sink);
+            if (c->input_path) rc = run_mmap(st, map, n, cs, sink, span_pipe);
+            else rc = run_stream(st, 0, cs, (size_t)c->threads, sink, span_pipe);
         }
     }
     stamp("chunks written");
@@ -623,6 +763,7 @@ int run(const blt_run_config* c) {
         if (::close(ofd) != 0) rc = os_error(errno);
     }
     stamp("output closed");
+    if (!rc) blt_log::emit(blt_log::kInfo, span.c_str(), "blt_core", "Tokenizer run completed successfully");
     return rc;
 }
 

@@ -10,15 +10,9 @@ constexpr uint64_t kTilePos = 4 * 512 * 16;   // positions per look-back tile (k
 constexpr uint64_t kTilePosU16 = kTilePos;     // positions per look-back tile of the generic u16 pass
 // (16384 measured and rejected: no VGPR spills, but twice the tiles and look-backs; f2 chain
 // 0.672 -> 0.804 ms, selfval 1.39 -> 1.77, multi 0.537 -> 0.575; profiles/r04_shift16_ab.txt)
-#ifndef BLT_TILE_TOK
-#define BLT_TILE_TOK 32768
-#endif
-constexpr uint64_t kTilePosTok = BLT_TILE_TOK;  // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
+constexpr uint64_t kTilePosTok = 32768;        // tokens per look-back tile of the u16 scan kernel (32 wave ranges)
 constexpr uint64_t kTokRange = 1024;           // tokens per wave range (one chunk-map word each)
-#ifndef BLT_TILE_BYTES
-#define BLT_TILE_BYTES 32768
-#endif
-constexpr uint64_t kTilePosBytes = BLT_TILE_BYTES;   // positions per look-back tile of the byte-input pass
+constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile of the byte-input pass
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 constexpr uint32_t kCtlLeft = 15;             // ctl word: workgroups of a single-pass launch that have left
@@ -74,10 +68,6 @@ struct PassParams {
                                // refuse (error bit 32, no output) when ntiles > ctl[kCtlCover]
     uint32_t* fused_fail;      // fused passes 1 + 2: set to 1 when a wave range's halo holds no
                                // restart (the host then runs the two-kernel chain instead)
-    uint64_t* status2;         // chain launches: the second status area (passes alternate; [ntiles])
-    uint32_t* pass_ctr;        // chain launches: per pass [2 i] tile ticket, [2 i + 1] tiles emitted;
-                               // zeroed by the chunk-map kernel ahead of the launch
-    uint32_t npasses;          // chain launches: u16 passes pass_id .. pass_id + npasses - 1
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
@@ -99,14 +89,6 @@ constexpr uint32_t kDoneBytePass = 0x80000000u;
 // p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
 // at least kTokRange tokens.
 hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
-// u16 passes p.pass_id .. p.pass_id + p.npasses - 1 of a general map in one launch
-// (seg::scan_tokens_kernel<kHash, false, true>), each as launch_scan_tokens would run it: the first
-// pass's chunk map kernel (which also zeroes p.pass_ctr), then one persistent launch whose passes
-// meet at a counter of emitted tiles.  Needs p.nchunks <= kChainMaxChunks (chunk starts in LDS),
-// every chunk at least kTokRange tokens in every pass, and p.status2 beside p.status.
-hipError_t launch_scan_chain(const PassParams& p, int device, hipStream_t s);
-constexpr uint64_t kChainMaxChunks = 1024;
-constexpr uint32_t kChainMaxPasses = 64;
 // Passes 1 and 2 of a general map in one kernel (seg::scan_tokens_kernel<kHash, true>): bytes in,
 // the second pass's big-endian tokens out, for maps whose bucket table fits in LDS and chunk sizes
 // >= kMinChunkBytes.  A wave range takes the first pass's carry-in from the 64 bytes before it
@@ -165,9 +147,17 @@ struct SparseParams {
     uint32_t* ticket;           // compaction tile ticket (zeroed)
     uint32_t* ctl;              // the chain's control block (error flags)
     uint32_t* sticky;
+    uint32_t* sample;           // detect's gate: mergeable pairs among kSparseSample sampled positions
+                                // (zeroed; null: no gate)
 };
 constexpr uint64_t kSparseTile = 16384;   // positions per compaction tile
-// detect: the first pass's seeds (every mergeable pair's first position) into seeds_in / bits_in
+// Positions the detect gate samples: kSparseSampleBlocks evenly spaced runs of 8192 positions.
+constexpr uint32_t kSparseSampleBlocks = 64;
+constexpr uint32_t kSparseSample = kSparseSampleBlocks * 8192u;
+// detect: the first pass's seeds (every mergeable pair's first position) into seeds_in / bits_in.
+// With q.sample, a sampling kernel runs first, and detect leaves the run not taken (flags 3, no
+// bitmaps) when the sample predicts more than half the lists' capacity of seeds: a dense cyclic map
+// goes on with the full passes for the cost of a few empty launches.
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s);
 // the first pass's seed list from the detect kernel's bitmap (q.seeds_out, q.nseeds_out)
 hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s);

@@ -63,10 +63,7 @@ constexpr uint32_t kSpinTimeoutTicks = 20000000u;   // 200 ms at 100 MHz
 // The clock is read once per kSpinClockEvery waits: s_memrealtime is a scalar-memory read, and
 // waiting for it (lgkmcnt, the counter LDS reads share) on every spin made each wait's polling
 // coarser: measured, the byte pass 8 % slower on cfg3 with a read per spin.
-#ifndef BLT_SPIN_EVERY
-#define BLT_SPIN_EVERY 64
-#endif
-constexpr uint32_t kSpinClockEvery = BLT_SPIN_EVERY;
+constexpr uint32_t kSpinClockEvery = 64;
 struct SpinClock {
     uint32_t t0 = 0;   // low half of the clock (wraps every 43 s; the deltas here are far shorter)
     uint32_t n = 0;
@@ -202,9 +199,6 @@ __device__ void record_error(const PassParams& p, uint32_t bit, uint32_t T, uint
 // agent-scope fence here writes back and invalidates the XCD's L2 under the workgroups still
 // running: measured, the kernel 75 us slower.)  flag: a workgroup-shared word the caller is done with.
 __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles, uint32_t* flag) {
-#ifdef BLT_NO_SELF_RESET   // experiment builds (tools/build_variant.sh): the kernel as before
-    return;
-#endif
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
     __syncthreads();
     if (threadIdx.x == 0)
@@ -229,29 +223,9 @@ __device__ __forceinline__ void self_reset(const PassParams& p, uint32_t ntiles,
 // read at the workgroup's start (written before the launch on its stream) and tested after the
 // table copy, off the critical path.  A relaxed atomic load, not a volatile one: measured, the
 // volatile load (which the backend orders with waits) made the headline byte pass 6 % slower
-// (cfg3 0.556 -> 0.590 ms, the check compiled out 0.554; BLT_COVER_LOAD switches for A/B).
-// u16 ranges with no merge emitted from registers (emit_shift16).  Off: measured slower
-// (profiles/r04_shift16_ab.txt): selfval, whose late passes it targets, 1.38 -> 1.54 ms with the
-// first version; with the head/tail stores folded into one loop every f2 row lost, also rows that
-// never take the path (chain 0.669 -> 0.800 ms, multi 0.535 -> 0.72): the extra code costs the
-// scan's registers and schedule more than the stage round trip it replaces.
-#ifndef BLT_SHIFT16
-#define BLT_SHIFT16 0
-#endif
-#ifndef BLT_SHIFT_DPP   // emit_shift16's fetch of the previous lane: DPP wave shift (1) or ds_bpermute (0)
-#define BLT_SHIFT_DPP 1
-#endif
-#ifndef BLT_COVER_LOAD
-#define BLT_COVER_LOAD 1
-#endif
+// (cfg3 0.556 -> 0.590 ms, the check compiled out 0.554).
 __device__ __forceinline__ uint32_t ws_cover(const PassParams& p) {
-#ifdef BLT_WS_NOCHECK   // (experiment: no coverage check)
-    return 0xFFFFFFFFu;
-#elif BLT_COVER_LOAD == 0
-    return p.ws_check ? *(const volatile uint32_t*)(p.ctl + kCtlCover) : 0xFFFFFFFFu;
-#else
     return p.ws_check ? __hip_atomic_load(p.ctl + kCtlCover, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0xFFFFFFFFu;
-#endif
 }
 __device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles, uint32_t cover) {
     if (ntiles <= cover) return false;
@@ -263,9 +237,6 @@ __device__ __forceinline__ bool ws_refused(const PassParams& p, uint32_t ntiles,
 // (a chunk or buffer end in a wave range) does not keep a per-lane constant live across the
 // byte pass's loop (the register allocator spilled two such VGPRs to scratch).
 __device__ __forceinline__ uint32_t lane16_here() {
-#ifdef BLT_NO_LANE16_ASM   // (A/B: the plain expression, which the compiler hoists)
-    return 16u * (threadIdx.x & 63u);
-#endif
     uint32_t l;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshlrev_b32 %0, 4, %0" : "=v"(l));
     return l;
@@ -411,12 +382,6 @@ template <> struct Seg<uint16_t> {
     static __device__ __forceinline__ uint32_t load1(const uint16_t* in, uint64_t pos) { return in[pos]; }
 };
 
-// u16 passes of merge_pass_body: chunk starts from an LDS list per tile (experiment switch: 0 walks
-// p.cstart from global memory as before)
-#ifndef BLT_BND_LDS
-#define BLT_BND_LDS 1
-#endif
-
 // Global -> LDS copy of n 16-byte units by nthr threads, kBatch loads in flight per thread
 // before their stores (a rolled loop waits for every load: one L2/MALL round trip each).
 template <int kBatch, typename T>
@@ -519,7 +484,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         // p.cstart as before.
         uint32_t nb = kThreads;
         uint64_t bk0 = 0;
-        if constexpr (!kDense && BLT_BND_LDS) {
+        if constexpr (!kDense) {
             if (p.cs == 0) {
                 (void)first_boundary(p, tile0, bk0);   // uniform: the same loads on every lane
                 const uint64_t k = bk0 + (uint64_t)tid;
@@ -779,7 +744,7 @@ __global__ __launch_bounds__(kThreads) void merge_tokens_kernel(PassParams p) {
 // per position into its wave's LDS stage (a consumed position writes the slot the next,
 // landing, position overwrites), and the wave copies the stage out with 16-byte buffer
 // stores; as a sub-tile is written its input registers are refilled with the next tile's
-// bytes.  The look-back reads 4 windows of 64 status words per round trip and folds them with
+// bytes.  The look-back reads a window of 64 status words per round trip and folds it with
 // ballots and a wave sum.
 // ===========================================================================================
 namespace seg {
@@ -831,27 +796,16 @@ __device__ __forceinline__ void add2(uint32_t& a, uint32_t bit) {
     asm("v_lshl_add_u32 %0, %1, 1, %0" : "+v"(a) : "v"(bit));
 }
 
-// Workgroup geometry: BLT_WAVES waves (16: 4 per SIMD, 128 VGPRs each; 8: 2 per SIMD, 256 VGPRs
-// each) times BLT_KS sub-tiles per wave make one 32 KiB tile.
-#ifndef BLT_WAVES
-#define BLT_WAVES 16
-#endif
+// Workgroup geometry: 16 waves (4 per SIMD, 128 VGPRs each) times 2 sub-tiles per wave make one
+// 32 KiB tile.
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr int kS = 2;                                  // sub-tiles per tile
 // Cache policy (buffer aux bits) of the input loads and the output stores: nt (2).  Every input
 // byte is read once by one CU and every output byte written once: cfg3 0.604-0.613 -> 0.597-0.599 ms,
 // cfg5 0.815-0.818 -> 0.804 ms (config_rates, same box); cfg2's 100 MiB, replayed back to back,
-// loses its cache residency (0.0937 -> 0.0955 ms).  0 = the default policy.
-#ifndef BLT_LDPOL
-#define BLT_LDPOL 2
-#endif
-#ifndef BLT_STPOL
-#define BLT_STPOL 2
-#endif
-#ifndef BLT_KS
-#define BLT_KS (32 / BLT_WAVES)
-#endif
-constexpr int kThreads = 64 * BLT_WAVES;
-constexpr int kWaves = kThreads / 64;
-constexpr int kS = BLT_KS;                             // sub-tiles per tile
+// loses its cache residency (0.0937 -> 0.0955 ms).
+constexpr int kLdPol = 2, kStPol = 2;
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
@@ -859,27 +813,10 @@ constexpr int kGroups = kS * kWaves;
 // 761 (2-byte aligned start + up to 1522 bytes), all the LDS the table leaves: every range of text
 // or random bytes under a large merge map (~580 tokens).  A range with more tokens goes through it
 // in two parts of 32 lanes (at most 512 tokens each).
-#ifndef BLT_STAGE_WAVE
-#define BLT_STAGE_WAVE (1536 * (16 / BLT_WAVES))
-#endif
-constexpr int kStageWave = BLT_STAGE_WAVE;    // the LDS the table leaves, shared by the waves
+constexpr int kStageWave = 1536;    // the LDS the table leaves, shared by the waves
 // Look-back windows of 64 status words per round trip.  (Measured: 2 or 4 windows cost more
 // through register spills than the extra round trips they save.)
-#ifndef BLT_LBWIN
-#define BLT_LBWIN 1
-#endif
-constexpr int kLbWin = BLT_LBWIN;
-// Phase-1 instruction grouping (experiment switches; 0: the compiler's schedule).
-#ifndef BLT_TOKSCHED
-#define BLT_TOKSCHED 0
-#endif
-#ifndef BLT_P1SCHED
-#define BLT_P1SCHED 0
-#endif
-// Look-backs publish the inclusive prefixes of the tiles they fold (win_upgrade).
-#ifndef BLT_LB_UPGRADE
-#define BLT_LB_UPGRADE 0
-#endif
+constexpr int kLbWin = 1;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 static_assert(kSubPos * kS == kTilePosBytes, "tile geometry");
 static_assert(kWavePos <= kMinChunkBytes, "at most one chunk end per wave sub-tile");
@@ -1096,21 +1033,6 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
         if (allm) m32 = 0x7FFF7FFFu;
         m[j] = (m32 & 0xFFFFu) | (m32 >> 15);
     }
-#if BLT_P1SCHED == 1
-    // experiment: both sub-tiles' addresses and table reads first (16 reads in flight per sub-tile)
-#pragma unroll
-    for (int j = 0; j < kS; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 33, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-    }
-#elif BLT_P1SCHED == 2
-    // experiment: reads in groups of 8, each behind the 16 address ops it needs
-#pragma unroll
-    for (int q = 0; q < 2 * kS; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 17, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-    }
-#endif
     // buffer end and chunk ends (uniform per wave range; rare)
     uint32_t bnext = ti.bge;   // first chunk start > the wave range's first position
 #pragma unroll
@@ -1173,15 +1095,18 @@ __device__ __forceinline__ void phase1_tile(uint32_t tab, const uint32_t (&x)[kS
 // kLive (u16 scan kernel): the groups' live bits (wfn[g][0] bit 1) are ORed into the tile's
 // status word and into tfn[0] bit 1.
 template <int NG = kGroups, bool kLive = false, bool kFresh = false>
-__device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane, const uint32_t (*wfn)[4],
+__device__ __forceinline__ void resolve_tile(const PassParams& p, uint32_t T, int lane_arg, const uint32_t (*wfn)[4],
                                              uint32_t (*gin)[4], uint32_t* tfn) {
+    // kFresh: the lane index computed here (a hoisted lane * 16 LDS offset was spilled, and its
+    // reload's vmcnt wait made the tile resolve wait for the next tile's loads)
+    const int lane = kFresh ? (int)(lane16_here() >> 4) : lane_arg;
     uint32_t gi = 1, gco = 0, g0 = 0, g1 = 0;
     if (lane < NG) { gi = wfn[lane][0]; gco = wfn[lane][1]; g0 = wfn[lane][2]; g1 = wfn[lane][3]; }
     const uint32_t tlive = kLive ? (__ballot((gi >> 1) & 1u) != 0) : 0u;
     if (kLive) gi &= 1u;
     const uint64_t nonid = __ballot(!gi);
     const uint64_t cmask = __ballot(gco);
-    const uint64_t below = nonid & ((1ull << (kFresh ? lane16_here() >> 4 : (uint32_t)lane)) - 1ull);   // (kFresh: lb_issue)
+    const uint64_t below = nonid & ((1ull << (uint32_t)lane) - 1ull);
     const uint32_t hb = below != 0;
     const uint32_t bc = hb ? (uint32_t)((cmask >> (63 - __clzll(below))) & 1ull) : 0u;
     const uint32_t cin0 = hb ? bc : 0u, cin1 = hb ? bc : 1u;
@@ -1243,12 +1168,12 @@ __device__ __forceinline__ void lb_issue(const PassParams& p, int64_t k, int lan
 }
 
 // Function of the aggregates in lanes [0, lim) of one window (lane 0 newest) applied to
-// carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.  With `lane_cin`
-// / `lane_scan` it also gives each lane its tile's carry-in and the inclusive (lane 0 up) scan of
-// the lanes' counts (for win_upgrade).
-__device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uint32_t c, uint64_t& tot,
-                                              uint32_t& live, uint32_t* lane_cin = nullptr,
-                                              uint32_t* lane_scan = nullptr) {
+// carry-in c (into the oldest): returns the carry-out and adds the tokens to `tot`.
+// kFresh (the u16 scan kernel): the lane index computed here (see lb_issue).
+template <bool kFresh = false>
+__device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane_arg, uint32_t c, uint64_t& tot,
+                                              uint32_t& live) {
+    const int lane = lane_arg;   // (kFresh: see lb_issue; measured here it cost more spills)
     const bool in = lane < lim;
     live |= __ballot(in && (s & kStLiveAgg) != 0) != 0;
     const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
@@ -1272,32 +1197,7 @@ __device__ __forceinline__ uint32_t win_apply(uint64_t s, int lim, int lane, uin
     const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x1FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
     const uint32_t scan = wave_scan(cnt);
     tot += lane_u32(scan, 63);
-    if (lane_cin) { *lane_cin = cin; *lane_scan = scan; }
     return nonid ? (uint32_t)((comask >> __builtin_ctzll(nonid)) & 1ull) : c;
-}
-
-// Inclusive-prefix upgrade (round 4).  A look-back that found the inclusive prefix of lane lim's
-// tile (offset obase, live bit lbase) and folded the aggregates of lanes [0, lim) knows the
-// inclusive prefix of every one of those tiles too, and publishes it for each lane whose word is
-// still an aggregate: one masked 8-byte store per lane, the same value the tile's owner publishes
-// after its own look-back (the prefix is a function of the input alone), so racing writers agree and
-// a word only ever moves from aggregate to inclusive.  Without it the nearest inclusive prefix lies
-// where the previous generation of tiles left one (every tile of the current one looks back at
-// about the same time): 18 tiles back on average on cfg3, and 45 % of look-backs found none in 64
-// and paid another status round trip.  kBase: tile index of lane 0.
-__device__ __forceinline__ void win_upgrade(const PassParams& p, uint64_t s, int lim, int lane, int64_t kbase,
-                                            uint64_t obase, uint32_t lbase, uint32_t cin, uint32_t scan) {
-    const bool in = lane < lim;
-    const uint32_t hi = (uint32_t)(s >> 32), lo = (uint32_t)s;
-    const uint32_t cnt = in ? (cin ? __builtin_amdgcn_alignbit(hi, lo, 30) & 0x1FFFFFFFu : lo & 0x3FFFFFFFu) : 0u;
-    const uint32_t total = lane_u32(scan, 63);
-    const uint32_t suffix = total - scan + cnt;   // tokens of lanes [lane, lim): this tile and the older ones
-    const bool ident = ((hi >> 28) & 3u) == 2u;
-    const uint32_t cout = ident ? cin : (hi >> 28) & 1u;   // a non-identity function is constant
-    const uint64_t lmask = __ballot(in && (s & kStLiveAgg) != 0);
-    const bool live = lbase || (lmask >> lane) != 0;
-    if (in && (s >> 62) == 1u)
-        st_publish(p.status + (kbase - lane), st_incl(cout, obase + suffix) | (live ? kStLiveIncl : 0ull));
 }
 
 struct TileFn {   // carry-in c -> (carry-out co_c, tokens t_c); selects, never indexed (no alloca)
@@ -1361,7 +1261,7 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 uint32_t c = (uint32_t)h;
                 uint64_t t = 0;
 #pragma unroll
-                for (int q = kLbWin - 1; q >= 0; --q) c = win_apply(s[q], 64, lane, c, t, live);
+                for (int q = kLbWin - 1; q >= 0; --q) c = win_apply<kFresh>(s[q], 64, lane, c, t, live);
                 t += c ? acc.t1 : acc.t0;
                 if (h == 0) { w.co0 = c ? acc.co1 : acc.co0; w.t0 = t; }
                 else { w.co1 = c ? acc.co1 : acc.co0; w.t1 = t; }
@@ -1381,18 +1281,10 @@ __device__ void lb_finish(const PassParams& p, uint32_t Tp, int lane, uint64_t (
                 const uint64_t sf = ((uint64_t)lane_u32((uint32_t)(s[q] >> 32), f) << 32) | lane_u32((uint32_t)s[q], f);
                 c = (uint32_t)(sf >> 61) & 1u;
                 off = sf & (kStLiveIncl - 1ull);
-                const uint32_t lbase = (sf & kStLiveIncl) != 0;
-                live |= lbase;
-                if (BLT_LB_UPGRADE && f > 0) {
-                    const uint64_t obase = off;
-                    uint32_t cin, scan;
-                    c = win_apply(s[q], f, lane, c, off, live, &cin, &scan);
-                    win_upgrade(p, s[q], f, lane, k - 64 * q, obase, lbase, cin, scan);
-                } else {
-                    c = win_apply(s[q], f, lane, c, off, live);
-                }
+                live |= (sf & kStLiveIncl) != 0;
+                c = win_apply<kFresh>(s[q], f, lane, c, off, live);
             } else {
-                c = win_apply(s[q], 64, lane, c, off, live);
+                c = win_apply<kFresh>(s[q], 64, lane, c, off, live);
             }
         }
         O = off + (c ? acc.t1 : acc.t0);
@@ -1431,8 +1323,6 @@ __device__ __forceinline__ u32x4 block_of(const u32x4& a, const u32x4& b, uint32
 // (rg = 0: every tile of a dense text emits a multiple of 8 tokens) that is the whole emission;
 // otherwise lane 0 stores the head of its block (its first 8 - rg/2 tokens) and lane 63 the block
 // after the range (its last rg/2 tokens) token by token.
-// kPol / kPol16: cache policy of the 16-byte and the 2-byte stores (chain launches: sc1, 16)
-template <int kPol = BLT_STPOL, int kPol16 = 0>
 __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, uint32_t rg, __amdgpu_buffer_rsrc_t ro,
                                            uint32_t ab, int lane) {
     const uint32_t sel = c ? 0x05040100u : 0x07060302u;   // low halves (c = 1) or high halves (c = 0)
@@ -1441,7 +1331,7 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q) P[q] = __builtin_amdgcn_perm(v[2 * q + 1], v[2 * q], sel);
     const uint32_t o = ab + 16u * (uint32_t)lane;
     if (rg == 0) {
-        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, kPol);
+        __builtin_amdgcn_raw_buffer_store_b128(P, ro, (int)o, 0, kStPol);
         return;
     }
     u32x4 Q;   // lane l - 1's tokens
@@ -1449,15 +1339,15 @@ __device__ __forceinline__ void emit_dense(const uint32_t (&v)[8], uint32_t c, u
     for (int q = 0; q < 4; ++q)
         Q[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)P[q], (int)P[q], 0x138, 0xF, 0xF, false);
     const uint32_t off = 16u - rg;
-    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, kPol);
+    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(block_of(Q, P, off >> 2, off & 3u), ro, (int)o, 0, kStPol);
     if (lane == 0 || lane == 63) {
         const uint32_t h = 8u - (rg >> 1);   // tokens of this lane in its own block
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint16_t tok = (uint16_t)(P[k >> 1] >> (16 * (k & 1)));
-            if (lane == 0 && (uint32_t)k < h) __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, kPol16);
+            if (lane == 0 && (uint32_t)k < h) __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + rg + 2u * k), 0, 0);
             if (lane == 63 && (uint32_t)k >= h)
-                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 1024u + 2u * (k - h)), 0, kPol16);
+                __builtin_amdgcn_raw_buffer_store_b16(tok, ro, (int)(ab + 1024u + 2u * (k - h)), 0, 0);
         }
     }
 }
@@ -1514,13 +1404,10 @@ struct CopyData {
     u32x4 vb[NB];
     uint16_t vf;
 };
-// BLT_OOB_COPY: the byte pass's copy-out reads and stores run on every lane, with lanes that have
-// nothing to store given an offset past the buffer (the store is dropped) instead of a branch
-// around the instruction: a v_cndmask per instruction instead of an exec save / branch / restore
-// (measured: cfg2 -1.5 %, cfg5 -0.5 %; the u16 pass's 3-block copy-out keeps its branches).
-#ifndef BLT_OOB_COPY
-#define BLT_OOB_COPY 1
-#endif
+// The byte pass's copy-out reads and stores run on every lane, with lanes that have nothing to
+// store given an offset past the buffer (the store is dropped) instead of a branch around the
+// instruction: a v_cndmask per instruction instead of an exec save / branch / restore (measured:
+// cfg2 -1.5 %, cfg5 -0.5 %; the u16 pass's 3-block copy-out keeps its branches: kOob = false).
 constexpr uint32_t kOobOff = 0x80000000u;   // >= every buffer resource's num_records (clamped to 2^31 - 1)
 template <int NB>
 __device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c, int lane, CopyData<NB>& d) {
@@ -1530,7 +1417,7 @@ __device__ __forceinline__ void copy_read(const uint8_t* stg, const CopyPart& c,
     const uint32_t of = lane < 8 ? c.rgp + 2u * (uint32_t)lane : tbeg + 2u * (uint32_t)(lane - 8);
     const bool bf = lane < 16 && of < (lane < 8 ? hend : c.re);
     const uint8_t* sp = stg;
-    if (BLT_OOB_COPY) {   // unconditional LDS reads inside the workgroup's LDS (junk where not stored)
+    {   // unconditional LDS reads inside the workgroup's LDS (junk where not stored)
 #pragma unroll
         for (int q = 0; q < NB; ++q)
             d.vb[q] = *reinterpret_cast<const u32x4*>(sp + min(hend + 16u * lane + 1024u * q, (uint32_t)kStageWave - 16u));
@@ -1564,7 +1451,7 @@ __device__ __forceinline__ void copy_read_pad(const uint8_t* arr, uint32_t x0, c
     }
     d.vf = bf ? *reinterpret_cast<const uint16_t*>(arr + stage_phys(x0 + of)) : (uint16_t)0;
 }
-template <int NB, bool kOob = BLT_OOB_COPY != 0, int kPol = BLT_STPOL, int kPol16 = 0>
+template <int NB, bool kOob = true>
 __device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const CopyPart& c, int lane, const CopyData<NB>& d) {
     const uint32_t hend = ((c.rgp + 15u) & ~15u) < c.re ? ((c.rgp + 15u) & ~15u) : c.re;
     const uint32_t tbeg = (c.re & ~15u) > hend ? (c.re & ~15u) : hend;
@@ -1575,16 +1462,16 @@ __device__ __forceinline__ void copy_store(__amdgpu_buffer_rsrc_t ro, const Copy
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             const uint32_t o = (uint32_t)lane + 64u * q < nfull ? c.abp + hend + 16u * lane + 1024u * q : kOobOff;
-            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)o, 0, kPol);
+            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)o, 0, kStPol);
         }
-        __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(bf ? c.abp + of : kOobOff), 0, kPol16);
+        __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(bf ? c.abp + of : kOobOff), 0, 0);
         return;
     }
 #pragma unroll
     for (int q = 0; q < NB; ++q)
         if ((uint32_t)lane + 64u * q < nfull)
-            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, kPol);
-    if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, kPol16);
+            __builtin_amdgcn_raw_buffer_store_b128(d.vb[q], ro, (int)(c.abp + hend + 16u * lane + 1024u * q), 0, kStPol);
+    if (bf) __builtin_amdgcn_raw_buffer_store_b16(d.vf, ro, (int)(c.abp + of), 0, 0);
 }
 
 // Sparse wave range: per-lane landing mask and token offset, the range's token count.
@@ -1683,7 +1570,7 @@ __device__ __forceinline__ void load_tile(const PassParams& p, uint32_t Tn, uint
 #pragma unroll
     for (int j = 0; j < kS; ++j) {
         const uint32_t wrel = (uint32_t)j * (uint32_t)kSubPos + wave * kWavePos;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, BLT_LDPOL);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)wrel + 16 * lane, 0, kLdPol);
         x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
         // the byte after the range, as its whole (4-aligned) dword: a u8 load would be masked
         // right here, which makes the compiler wait for it.  The range check covers voffset
@@ -1785,9 +1672,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     const uint32_t allm = uni(p.allm), mark = uni(p.mark);
     const bool has_coff = p.chunk_off != nullptr;   // (the pointer itself is reloaded where stored)
 
-#if BLT_COVER_LOAD != 2
     const uint32_t cover = ws_cover(p);
-#endif
     // timing build: workgroup start, table copied, exit (s_memrealtime) after the per-tile records
     uint64_t* const wg_rec = (kTiming && p.debug) ? p.debug + (8ull + 8ull * kWaves) * p.ntiles + 4ull * blockIdx.x : nullptr;
     if (wg_rec && tid == 0) wg_rec[0] = __builtin_amdgcn_s_memrealtime();
@@ -1822,9 +1707,6 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
     uint32_t T = uni(s_tk[kRing - 2]);    // tile in phase 1
     uint32_t Tp = kNone;                  // tile waiting for emission
     uint32_t Tq = uni(s_tk[kRing - 1]);   // the tile after T (its bytes load during T's iteration)
-#if BLT_COVER_LOAD == 2
-    const uint32_t cover = ws_cover(p);
-#endif
     if (ws_refused(p, ntiles, cover)) T = kNone;   // (its two tickets are dropped: the reset zeroes them)
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     TInfo ti = {}, tip = {};
@@ -2067,7 +1949,6 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
     if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
-    if (p.pass_ctr && r < 2u * p.npasses) p.pass_ctr[r] = 0u;   // a chain launch's counters
     const uint64_t nc = p.nchunks;
     const bool in_lds = nc <= kCmLds;
     if ((uint64_t)blockIdx.x * 256u * kWavePos >= n) return;   // uniform: no range of this block is live
@@ -2084,14 +1965,12 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
 }
 
 // Tokens of tile Tn into x (the same straight-line loads as load_tile; near the buffer end the
-// lanes' tokens again one by one), and each wave range's chunk-map word (0 past the end).
+// lanes' tokens again one by one), and the wave ranges' chunk-map words, packed in one register:
+// lane l holds dword l & 1 of sub-tile (l >> 1) & 1's word (read back with v_readlane where used;
+// a wave-uniform value in a VGPR of its own per dword was 8 registers the kernel does not have).
 // Sub-tile j of wave w: tokens [j kSubTok + 1024 w, +1024), wave range Tn kGroupsTok + j kWaves + w.
-// kChain (chain launches): every load sc1 (the tokens were written by this launch's previous pass,
-// write-through), and no chunk-map words (the caller derives them from the chunk starts in LDS).
-template <bool kChain = false>
 __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32_t Tn, uint32_t wave, int lane,
-                                         uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2]) {
-    constexpr int kPol = kChain ? 16 : BLT_LDPOL, kPol2 = kChain ? 16 : 0;
+                                         uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t& cw) {
     const uint8_t* in = reinterpret_cast<const uint8_t*>(p.in);
     const uint64_t tile0 = (uint64_t)Tn * kTileTok;
     const uint64_t left = n > tile0 ? n - tile0 : 0;
@@ -2102,16 +1981,15 @@ __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32
     for (int j = 0; j < kSt; ++j) {
         const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
         const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
-        const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, kPol);
-        const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, kPol);
+        const auto v0 = __builtin_amdgcn_raw_buffer_load_b128(rd, o, 0, kLdPol);
+        const auto v1 = __builtin_amdgcn_raw_buffer_load_b128(rd, o + 16, 0, kLdPol);
         x[j][0] = v0[0]; x[j][1] = v0[1]; x[j][2] = v0[2]; x[j][3] = v0[3];
         x[j][4] = v1[0]; x[j][5] = v1[1]; x[j][6] = v1[2]; x[j][7] = v1[3];
-        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, kPol2);
-        if constexpr (!kChain) {
-            const auto c = __builtin_amdgcn_raw_buffer_load_b64(rm, (int)(8 * ((uint32_t)j * kWaves + wave)), 0, 0);
-            cw[j][0] = c[0]; cw[j][1] = c[1];
-        }
+        nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(2 * (wrel + kWavePos)), 0, 0);
     }
+    static_assert(kSt == 2, "chunk-map words: 4 dwords per wave");
+    const uint32_t cl = (lane16_here() >> 4) & 3u;
+    cw = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rm, (int)(8u * ((cl >> 1) * (uint32_t)kWaves + wave) + 4u * (cl & 1u)), 0, 0);
     const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
 #pragma unroll
     for (int j = 0; j < kSt; ++j) {
@@ -2119,11 +1997,11 @@ __device__ __forceinline__ void load_tok(const PassParams& p, uint64_t n, uint32
         if (rn > wrel && rn - wrel < kWavePos + 16u) {   // uniform: the buffer end is near this range
             const __amdgpu_buffer_rsrc_t r = rsrc_at(in + 2 * tile0, 2 * left);
             const int o = 2 * (int)(wrel + 16u * (uint32_t)lane);
-            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, kPol2);
+            nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(2 * (wrel + kWavePos)), 0, 0);
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                x[j][q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, kPol2) |
-                          ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, kPol2) << 16);
+                x[j][q] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q, 0, 0) |
+                          ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 4 * q + 2, 0, 0) << 16);
         }
     }
 }
@@ -2174,12 +2052,6 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
         const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
         r[k] = tok_get<kHash>(p, tab, key);
     }
-#if BLT_TOKSCHED
-    if constexpr (kHash == 2) {   // experiment: the keys and bucket addresses, then all 16 bucket reads
-        __builtin_amdgcn_sched_group_barrier(0x002, 56, 1);
-        __builtin_amdgcn_sched_group_barrier(0x100, 16, 1);
-    }
-#endif
     uint32_t racc = 0;
 #pragma unroll
     for (int k = 0; k < 16; k += 2) racc |= r[k] | r[k + 1];
@@ -2195,12 +2067,13 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
     uint32_t m = (m32 & 0xFFFFu) | (m32 >> 15);
     const bool has_end = (cwl & kCmEnd) != 0u;
     if (rem <= kWavePos || has_end) {   // uniform; rare
-        const int32_t rr = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - 16 * lane;
+        const uint32_t l16 = lane16_here();   // (not a hoisted per-lane constant: see lane16_here)
+        const int32_t rr = (int32_t)(rem > 2u * kWavePos ? 2u * kWavePos : rem) - (int32_t)l16;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
         uint32_t mm = m & (next_ok ? vmask : ((vmask >> 1) | (rr > 16 ? 0x8000u : 0u)));
         uint32_t forced = (!next_ok && rr >= 1 && rr <= 16) ? (1u << (rr - 1)) : 0u;   // the buffer's last token
         if (has_end) {                                                     // a chunk's last token
-            const uint32_t e = ((cwl >> 12) & 0x7FFu) - 16u * (uint32_t)lane;
+            const uint32_t e = ((cwl >> 12) & 0x7FFu) - l16;
             if (e < 16u) { mm &= ~(1u << e); forced |= 1u << e; }
         }
         if (__ballot(forced != 0)) {   // a cut merge emits its own token
@@ -2213,14 +2086,11 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
         }
         m = mm;
         st.mv[j] = mm | (vmask << 16);
-        // only the merges that survive the buffer and chunk ends count: look them up again
+        // only the merges that survive the buffer and chunk ends count (their lookups, still live:
+        // a second lookup here, sixteen results in flight, made the kernel spill)
         uint32_t lacc = 0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int h = k >> 1;
-            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nbw, x[h], 2) : x[h];
-            if ((mm >> k) & 1u) lacc |= tok_get<kHash>(p, tab, key);
-        }
+        for (int k = 0; k < 16; ++k) lacc |= ((mm >> k) & 1u) ? r[k] : 0u;
         lv = (lacc >> 30) & 1u;
     } else {
         st.mv[j] = m | 0xFFFF0000u;
@@ -2229,84 +2099,16 @@ __device__ __forceinline__ uint32_t phase1_tok(const PassParams& p, uint32_t tab
     return m;
 }
 
-// A u16 wave range none of whose pairs merged (every position lands): its 1024 tokens go out as
-// they are, shifted to the range's output offset, straight from registers.  Lane l holds output
-// bytes [32 l, 32 l + 32) of the range (v[0..7]), at byte rg + 32 l past the 16-byte boundary ab;
-// it stores aligned blocks 2 l (lane l - 1's last rg bytes, then its own first 16 - rg: one DPP
-// fetch of the previous lane's registers) and 2 l + 1 (its own).  Lane 0 stores the head of block 0
-// and lane 63 the partial block 128 token by token, as emit_dense does.  (A general map's late
-// passes, e.g. the self-valued map's, merge a few pairs in 256 MiB: nearly every range used to take
-// the stage round trip, 16 ds_write_b16 per lane, only to copy its tokens one slot to the left.)
-// Aligned blocks 2 l and 2 l + 1 from the 64-byte concatenation w (lane l - 1's bytes, then lane
-// l's) at byte offset 4 D + r (D compile-time: the shift has four cases, one per dword).
-template <int D>
-__device__ __forceinline__ void shift_blocks(const uint32_t (&w)[16], uint32_t r, u32x4& B0, u32x4& B1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        B0[q] = funnel(w[D + q + 1], w[D + q], r);
-        B1[q] = funnel(w[D + q + 5], w[D + q + 4], r);
-    }
-}
-template <int kPol = BLT_STPOL, int kPol16 = 0>
-__device__ __forceinline__ void emit_shift16(const uint32_t (&v)[8], uint32_t rg, __amdgpu_buffer_rsrc_t ro,
-                                             uint32_t ab, int lane) {
-    const uint32_t o = ab + 32u * (uint32_t)lane;
-    if (rg == 0) {   // uniform
-        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[0], v[1], v[2], v[3]}, ro, (int)o, 0, kPol);
-        __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[4], v[5], v[6], v[7]}, ro, (int)(o + 16u), 0, kPol);
-        return;
-    }
-    uint32_t w[16];   // lane l - 1's 32 bytes, then lane l's
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-#if BLT_SHIFT_DPP
-        w[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[q], (int)v[q], 0x138, 0xF, 0xF, false);
-#else
-        w[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (lane > 0 ? lane - 1 : 0), (int)v[q]);
-#endif
-        w[8 + q] = v[q];
-    }
-    // block 2 l = concatenation bytes [32 - rg, 48 - rg), block 2 l + 1 = [48 - rg, 64 - rg)
-    const uint32_t b0 = 32u - rg, d = b0 >> 2, r = b0 & 3u;   // uniform: d in 4..7, r in {0, 2}
-    u32x4 B0, B1;
-    if (d == 4) shift_blocks<4>(w, r, B0, B1);
-    else if (d == 5) shift_blocks<5>(w, r, B0, B1);
-    else if (d == 6) shift_blocks<6>(w, r, B0, B1);
-    else shift_blocks<7>(w, r, B0, B1);
-    if (lane != 0) __builtin_amdgcn_raw_buffer_store_b128(B0, ro, (int)o, 0, kPol);
-    __builtin_amdgcn_raw_buffer_store_b128(B1, ro, (int)(o + 16u), 0, kPol);
-    // lane 0: its first h0 = (16 - rg) / 2 tokens at ab + rg; lane 63: its last h63 = rg / 2 at
-    // ab + 2048; both in the same store instructions (h0 + h63 = 8: at most 7 of them)
-    const uint32_t h0 = (16u - rg) >> 1, h63 = rg >> 1, hm = h0 > h63 ? h0 : h63;
-    if (lane == 0 || lane == 63) {
-        const uint32_t k0 = lane == 0 ? 0u : 16u - h63, hl = lane == 0 ? h0 : h63;
-        const uint32_t a0 = lane == 0 ? ab + rg : ab + 2048u;
-#pragma unroll
-        for (uint32_t k = 0; k < 7u; ++k) {
-            if (k >= hm) break;   // uniform
-            const uint32_t kk = k0 + k;
-            uint32_t wv = v[0];
-#pragma unroll
-            for (int q = 1; q < 8; ++q) wv = (kk >> 1) == (uint32_t)q ? v[q] : wv;
-            if (k < hl)
-                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(wv >> (16 * (kk & 1u))), ro, (int)(a0 + 2u * k), 0, kPol16);
-        }
-    }
-}
-
 // Emission of sub-tile j's wave range (as emit_tile), its chunk start from the chunk-map word.
 // rem: tokens from the range start to the buffer end; wtok: the range's first input token.
-// kChain (chain launches): every store sc1 (write-through: the next pass of the same launch reads
-// them on any XCD) and the chunk offsets from p (they alternate between passes).
-__device__ __forceinline__ void coff_store(uint64_t* a, uint64_t v, bool sc1) {
-    if (sc1) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *a = v;
-}
-template <bool kChain = false>
 __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uint32_t rem, uint32_t cwl, uint32_t cwh,
-                                         int lane, int j, const TileStateT<kSt>& st, const uint32_t* gin,
+                                         int, int j, const TileStateT<kSt>& st, const uint32_t* gin,
                                          uint32_t C, uint64_t O, uint8_t* stg, uint32_t wave, bool has_coff,
-                                         bool inplace = true, uint64_t* coff_chain = nullptr) {
+                                         bool inplace = true) {
+    // the lane index computed here (inline asm is never hoisted): the copy-out's per-lane offsets,
+    // hoisted out of the loop as constants, were spilled, and each reload's vmcnt wait made the
+    // emission wait for the next tile's loads
+    const int lane = (int)(lane16_here() >> 4);
     uint8_t* out = reinterpret_cast<uint8_t*>(p.out);
     const uint64_t obase = (2ull * O) & ~15ull;
     const uint32_t orel = (uint32_t)(2ull * O - obase);
@@ -2317,8 +2119,8 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const bool cstart = has_coff && (cwl & kCmStart) != 0u;
     if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
         // dense: every pair merges, so the only possible chunk start is the range's first token
-        if (cstart && lane == 0) coff_store((kChain ? coff_chain : KARG(chunk_off)) + cwh, O + goff, kChain);
-        emit_dense<kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
+        if (cstart && lane == 0) KARG(chunk_off)[cwh] = O + goff;
+        emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
     }
     const uint32_t m = st.mv[j] & 0xFFFFu, vmask = st.mv[j] >> 16;
@@ -2332,25 +2134,18 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     if (cstart) {
         const uint32_t e = (cwl & 0x7FFu) - lane16_here();
         if (e < 16u)
-            coff_store((kChain ? coff_chain : KARG(chunk_off)) + cwh, O + goff + lane_off + __popc(L & ((1u << e) - 1u)),
-                       kChain);
+            KARG(chunk_off)[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
     if (inplace && wcnt == (rem < kWavePos ? rem : kWavePos) && O + goff == wtok) return;
-#if BLT_SHIFT16
-    if (__ballot(L != 0xFFFFu) == 0) {   // every position lands: the tokens as they are, shifted
-        emit_shift16<kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(st.v[j], gb & 15u, ro, gb & ~15u, lane);
-        return;
-    }
-#endif
     // one part: the stage holds the range's at most 1024 tokens
     const uint32_t x0 = wave * (uint32_t)kStageTok;   // the wave's stage, logical bytes
     stage_b16_pad(st.v[j], L, stg, x0 + (gb & 15u) + 2u * lane_off);
     const CopyPart cp = {gb & ~15u, gb & 15u, (gb & 15u) + 2u * wcnt};
     CopyData<kCopyBlkTok> d;
     copy_read_pad(stg, x0, cp, lane, d);
-    copy_store<kCopyBlkTok, false, kChain ? 16 : BLT_STPOL, kChain ? 16 : 0>(ro, cp, lane, d);   // (branch-free here: f2 +2.5 %)
+    copy_store<kCopyBlkTok, false>(ro, cp, lane, d);   // (branch-free here: f2 +2.5 %)
 }
 
 // ===========================================================================================
@@ -2417,7 +2212,7 @@ __device__ __forceinline__ void load_fused(const PassParams& p, uint64_t n, uint
 #pragma unroll
     for (int j = 0; j < kSt; ++j) {
         const uint32_t wrel = (uint32_t)j * kSubTok + wave * kWavePos;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(wrel + 16u * (uint32_t)lane), 0, BLT_LDPOL);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(wrel + 16u * (uint32_t)lane), 0, kLdPol);
         x[j][0] = v[0]; x[j][1] = v[1]; x[j][2] = v[2]; x[j][3] = v[3];
         nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(wrel + kWavePos), 0, 0);
         const uint64_t wb = tile0 + wrel;
@@ -2579,54 +2374,12 @@ __device__ __forceinline__ void fused_front(const PassParams& p, uint32_t tab, u
     }
 }
 
-// Chunk-map words of a chain launch (no chunk_map_kernel between its passes): the wave range at
-// token lo from the pass's chunk starts in LDS (cs[0, nc), nc <= kCmLds; positions below 2^32, which
-// the host checks), the lower bound found by two ballots (blocks of 16 starts, then inside the
-// block) instead of a dependent search.  The same word as chunk_map_kernel's cm_word.
-__device__ __forceinline__ void lds_cm_word(const uint32_t* cs, uint32_t nc, uint32_t lo, int lane, uint32_t (&cw)[2],
-                                            bool& bad) {
-    const uint32_t i1 = (uint32_t)lane * 16u;
-    const uint32_t nb = __popcll(__ballot(i1 < nc && cs[i1 < nc ? i1 : 0u] < lo));   // blocks starting below lo
-    uint32_t a = 0;
-    if (nb != 0) {
-        const uint32_t base = (nb - 1u) * 16u, i2 = base + (uint32_t)lane;
-        a = base + __popcll(__ballot(lane < 16 && i2 < nc && cs[i2 < nc ? i2 : 0u] < lo));
-    }
-    a = uni(a);
-    const uint32_t hi = lo + (uint32_t)kWavePos;
-    uint32_t wl = 0, wh = 0;
-    const uint32_t ca = a < nc ? cs[a] : 0xFFFFFFFFu;
-    if (ca < hi) {
-        wl |= (ca - lo) | kCmStart;
-        wh = a;
-        bad |= a + 1u < nc && cs[a + 1u] < hi;
-    }
-    const uint32_t e = (a < nc && ca == lo) ? a + 1u : a;   // first chunk start > lo
-    const uint32_t ce = e < nc ? cs[e] : 0xFFFFFFFFu;
-    if (ce <= hi && ce != 0xFFFFFFFFu) {
-        wl |= ((ce - 1u - lo) << 12) | kCmEnd;
-        bad |= e + 1u < nc && cs[e + 1u] <= hi;
-    }
-    cw[0] = wl;
-    cw[1] = wh;
-}
-
-// kChain: one launch runs u16 passes p.pass_id .. p.pass_id + p.npasses - 1 of a general map
-// (launch_scan_chain).  Between passes the workgroups wait until every tile of the pass is emitted
-// (a counter per pass; every workgroup waiting has claimed no tile of the pass, and every claimed
-// tile belongs to a running workgroup, so the wait ends whatever else runs on the device), then
-// read the pass's count and done word and take the next pass's tickets; the map's table stays in
-// LDS.  Token, chunk-offset and count stores are sc1 (write-through) and the next pass's loads sc1
-// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores drained by each wave's vmcnt(0),
-// then one agent-scope add per tile, sc1 loads).  The passes alternate status areas (each pass
-// zeroes the next pass's word of every tile it resolves), totals and chunk-offset arrays exactly as
-// separate launches do, so the chain's host side and chain_final_kernel read the same words.
-template <int kHash, bool kFused = false, bool kChain = false>
+template <int kHash, bool kFused = false>
 __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
-    static_assert(!(kFused && kChain), "a chain launch runs u16 passes");
     constexpr bool kHashLds = kHash != 0;
     extern __shared__ __attribute__((aligned(16))) uint2 s_tokhash[];
     __shared__ __attribute__((aligned(16))) uint8_t s_stage[kWaves * kStageTokPhys];   // padded
+    
     __shared__ __attribute__((aligned(16))) uint32_t s_wfn[kRing][kGroupsTok][4];
     __shared__ uint32_t s_gin[kRing][kGroupsTok][4];
     __shared__ uint32_t s_tfn[kRing][4];
@@ -2635,19 +2388,16 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
     __shared__ uint32_t s_tk[kRing];
     __shared__ uint32_t s_p1cnt[kRing];
     __shared__ uint32_t s_rdone, s_lbdone, s_tkdone;
-    __shared__ uint32_t s_cs[kChain ? kCmLds : 1];   // chain: the pass's chunk starts (below 2^32)
-    __shared__ uint32_t s_emc[kRing];                // chain: waves done with each iteration's stores
-    __shared__ uint32_t s_tk0[2];                    // chain: a pass's first two tickets
 
     // an earlier pass merged nothing (uniform over the grid); both loads in flight together
     const bool done = !kFused && pass_done(p);
-    uint64_t n = kFused ? p.n : uni64(token_count(p));   // fused: bytes
+    const uint64_t n = kFused ? p.n : uni64(token_count(p));   // fused: bytes
     if (done) return;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wave = uni((uint32_t)tid >> 6);
     const bool has_coff = p.chunk_off != nullptr;
-    uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
+    const uint32_t ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
     // the grid was sized for the token bound; workgroups past the tiles the previous pass left leave
     // before copying the table (the ones below claim every ticket)
     if (blockIdx.x >= ntiles) return;
@@ -2673,100 +2423,58 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                     (__attribute__((address_space(3))) void*)(dst + u0), 16, 0, 0);
         }
     }
-    // ticket counter: the control block's, or a chain launch's per pass ([0] tickets, [1] tiles emitted)
-    // A chain launch's pass pi uses the kernel argument's arrays with the roles of each pair swapped
-    // when pi is odd (totals, chunk offsets, status areas; KARG reloads where used: nothing per pass
-    // is held in registers but pi and p.status, which the shared look-back helpers read).
-    uint32_t pi = 0;
-    auto sw = [&]() { return (pi & 1u) != 0u; };
-    auto tkp_of = [&]() { return kChain ? KARG(pass_ctr) + 2u * pi : p.ctl; };
-    uint32_t* tkp = tkp_of();
-    const uint32_t nc = kChain ? (uint32_t)p.nchunks : 0u;
-    // chain: the pass's chunk starts into LDS (sc1: the previous pass of this launch wrote them)
-    auto load_starts = [&]() {
-        const uint64_t* cst = sw() ? KARG(chunk_off) : KARG(cstart);
-        for (uint32_t i = (uint32_t)tid; i < nc; i += (uint32_t)kThreads)
-            s_cs[i] = (uint32_t)__hip_atomic_load(const_cast<uint64_t*>(cst) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
     if (tid == 0) {
-        s_tk0[0] = atomicAdd(tkp, 1u);
-        s_tk0[1] = atomicAdd(tkp, 1u);
-        for (int r = 0; r < kRing; ++r) { s_p1cnt[r] = 0; s_emc[r] = 0; }
+        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);   // T
+        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);   // Tq, the tile after it
+        for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
-    if constexpr (kChain) load_starts();
     __syncthreads();
     const uint32_t tab = kHashLds ? uni(lds_addr(s_tokhash)) : 0u;
-    uint32_t T = uni(s_tk0[0]);
+    uint32_t T = uni(s_tk[kRing - 2]);
     uint32_t Tp = kNone;
-    uint32_t Tq = uni(s_tk0[1]);
+    uint32_t Tq = uni(s_tk[kRing - 1]);
     if (T >= ntiles || Tq >= ntiles) Tq = kNone;
     __syncthreads();
-
-    // chain: chunk-map words of tile Tn's wave ranges from the chunk starts in LDS
-    auto chain_map = [&](uint32_t Tn, uint32_t (&cw)[kSt][2]) {
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < kSt; ++j)
-            lds_cm_word(s_cs, nc, Tn * kTileTok + (uint32_t)j * kSubTok + wave * kWavePos, lane, cw[j], bad);
-        if (bad && lane == 0) flag_error(p.ctl, KARG(sticky), 16u);   // chunks shorter than a wave range
-    };
     uint32_t it = 0;
-    // chain: the tile this wave emitted in the last iteration, whose stores the next vmcnt(0) wait
-    // completes; each wave then counts itself in s_emc, and the last of the 16 adds the tile to
-    // the pass's emitted counter
-    uint32_t Te = kNone;
-    bool sig_pending = false;
-    auto signal = [&]() {
-        const uint32_t e = it - 1u, es = e & (kRing - 1);
-        uint32_t old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(&s_emc[es], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        old = uni(old);
-        if (old == (uint32_t)kWaves * (e / kRing + 1u) - 1u && Te < ntiles && lane == 0)
-            __hip_atomic_fetch_add(tkp + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sig_pending = false;
-    };
 
-    for (;;) {   // passes: one, or a chain launch's npasses (per-pass state declared here,
-                 // so none of it is carried from one pass into the next)
-        uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca[kSt][2], cb[kSt][2];
+    {
+        uint32_t xa[kSt][8], xb[kSt][8], na[kSt], nb[kSt], ca = 0u, cb = 0u;
 #pragma unroll
-        for (int j = 0; j < kSt; ++j) { na[j] = nb[j] = 0u; ca[j][0] = ca[j][1] = cb[j][0] = cb[j][1] = 0u; }
+        for (int j = 0; j < kSt; ++j) na[j] = nb[j] = 0u;
+        
         if (T < ntiles) {
             if constexpr (kFused) load_fused(p, n, T, wave, lane, xa, na);
-            else if constexpr (kChain) load_tok<true>(p, n, T, wave, lane, xa, na, ca);
             else load_tok(p, n, T, wave, lane, xa, na, ca);
         }
         TileStateT<kSt> sa, sb;
         uint64_t lbs[kLbWin];
-        uint32_t cwp[kSt][2];   // Tp's chunk-map words
-#pragma unroll
-        for (int j = 0; j < kSt; ++j) cwp[j][0] = cwp[j][1] = 0u;
-        auto step = [&](uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t (&cw)[kSt][2], uint32_t (&xq)[kSt][8],
-                        uint32_t (&nxtq)[kSt], uint32_t (&cwq)[kSt][2], TileStateT<kSt>& sc, const TileStateT<kSt>& sp) {
+        uint32_t cwp = 0u;   // Tp's chunk-map words, packed as load_tok packs them
+        auto step = [&](uint32_t (&x)[kSt][8], uint32_t (&nxt)[kSt], uint32_t& cw, uint32_t (&xq)[kSt][8],
+                        uint32_t (&nxtq)[kSt], uint32_t& cwq, TileStateT<kSt>& sc, const TileStateT<kSt>& sp) {
             const uint32_t slot = it & (kRing - 1), pslot = (it - 1) & (kRing - 1);
+            // the lane index per iteration (inline asm is never hoisted): per-lane constants derived
+            // from it and hoisted out of the loop took the registers this kernel spilled (19-23 VGPRs
+            // at one point), and each reload's vmcnt wait held its phase for the next tile's loads
+            const int lane = (int)(lane16_here() >> 4);
             uint64_t stamp[7];
             const bool stamping = kTiming && p.debug != nullptr;
             if (stamping) stamp[0] = __builtin_amdgcn_s_memtime();
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): T's tokens and map words have landed
             if (stamping) stamp[1] = __builtin_amdgcn_s_memtime();
-            if constexpr (kChain) {
-                if (sig_pending) signal();   // (the wait above completed last iteration's stores)
-                if (T < ntiles) chain_map(T, cw);   // here, before Tq's loads are in flight: fewer live registers
-            }
+
             uint32_t cwl[kSt], cwh[kSt];
 #pragma unroll
             for (int j = 0; j < kSt; ++j) {
-                cwl[j] = kFused ? 0u : uni(cw[j][0]);   // fused: from the front end
-                cwh[j] = kFused ? 0u : uni(cw[j][1]);
+                cwl[j] = kFused ? 0u : lane_u32(cw, 2 * j);   // fused: from the front end
+                cwh[j] = kFused ? 0u : lane_u32(cw, 2 * j + 1);
             }
             if (Tq < ntiles) {
                 if constexpr (kFused) load_fused(p, n, Tq, wave, lane, xq, nxtq);
-                else if constexpr (kChain) load_tok<true>(p, n, Tq, wave, lane, xq, nxtq, cwq);
                 else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
             }
             uint32_t tk = kNone;
-            if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(tkp, 1u);
+            if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
             asm volatile("" ::: "memory");
 
             bool lbw = wave == 0;
@@ -2823,7 +2531,6 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 lbw = old == (uint32_t)kWaves * (it / kRing);
                 if (old == (uint32_t)kWaves * (it / kRing + 1u) - 1u) {
                     resolve_tile<kGroupsTok, true, true>(p, T, lane, s_wfn[slot], s_gin[slot], s_tfn[slot]);
-                    if (kChain && lane == 0) st_publish((sw() ? KARG(status) : KARG(status2)) + T, 0ull);   // the next pass's word of T
                     if (lane == 0) lds_release(&s_rdone, it + 1u);
                 }
             }
@@ -2856,16 +2563,9 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                         // component, so the next pass merges nothing (a pair of two tokens this pass
                         // left alone was looked up here and rejected; a new token is in no key).
                         const bool fixed = p.done && C <= 1u && (fin == n || !live);
-                        if constexpr (kChain) {   // sc1: the next pass of this launch reads them
-                            __hip_atomic_store(const_cast<uint64_t*>(sw() ? KARG(n_dev) : KARG(total)), fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            __hip_atomic_store(const_cast<uint64_t*>(sw() ? KARG(cstart) : KARG(chunk_off)) + KARG(nchunks), fin, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                            if (fixed) __hip_atomic_store(p.done, KARG(pass_id) + pi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        } else {
-                            *KARG(total) = fin;
-                            if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
-                            if (fixed) *p.done = p.pass_id;
-                        }
+                        *KARG(total) = fin;
+                        if (uint64_t* co = KARG(chunk_off)) co[KARG(nchunks)] = fin;
+                        if (fixed) *KARG(done) = KARG(pass_id);   // (reloaded: kept live, it was spilled)
                     }
                     if (kDebugRecord && p.debug) {
                         uint64_t* d = p.debug + 4ull * Tp;
@@ -2888,9 +2588,8 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
 #pragma unroll
                     for (int j = 0; j < kSt; ++j) {
                         const uint64_t wtok = (uint64_t)Tp * kTileTok + (uint64_t)j * kSubTok + wave * kWavePos;
-                        emit_tok<kChain>(p, wtok, kFused ? 0u : rem_of(Tp, j), cwp[j][0], cwp[j][1], lane, j, sp,
-                                         s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff, !kFused,
-                                         kChain ? const_cast<uint64_t*>(sw() ? KARG(cstart) : KARG(chunk_off)) : nullptr);
+                        emit_tok(p, wtok, kFused ? 0u : rem_of(Tp, j), lane_u32(cwp, 2 * j), lane_u32(cwp, 2 * j + 1), lane, j, sp,
+                                 s_gin[pslot][(uint32_t)j * kWaves + wave], Cp, Op, s_stage, wave, has_coff, !kFused);
                     }
                 }
                 __builtin_amdgcn_s_setprio(0);
@@ -2912,11 +2611,11 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
 #pragma unroll
                 for (int q = 0; q < 6; ++q) w[q] = stamp[q + 1] - stamp[q];
             }
-#pragma unroll
-            for (int j = 0; j < kSt; ++j) { cwp[j][0] = cwl[j]; cwp[j][1] = cwh[j]; }
-            if constexpr (kChain) {
-                Te = Tp;   // emitted (or failed) in this iteration: counted once its stores complete
-                sig_pending = true;
+            if constexpr (kFused) {   // (the front end's words, packed as load_tok packs them)
+                const uint32_t cl = (lane16_here() >> 4) & 3u;
+                cwp = cl == 0u ? cwl[0] : cl == 1u ? cwh[0] : cl == 2u ? cwl[1] : cwh[1];
+            } else {
+                cwp = cw;
             }
             Tp = T;
             T = Tq;
@@ -2928,52 +2627,6 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
             step(xa, na, ca, xb, nb, cb, sa, sb);
             if (!(T < ntiles || Tp < ntiles)) break;
             step(xb, nb, cb, xa, na, ca, sb, sa);
-        }
-        if constexpr (!kChain) {
-            break;
-        } else {
-            // the pass's last stores of this wave, counted; then every tile of the pass emitted
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-            if (sig_pending) signal();
-            if (tid == 0) {
-                SpinClock clk;
-                while (__hip_atomic_load(tkp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles) {
-                    if (clk.expired()) {
-                        flag_error(p.ctl, KARG(sticky), 8u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            __syncthreads();
-            if (pi + 1u >= KARG(npasses)) break;
-            // the next pass: its input count and offsets are this pass's outputs (the arrays
-            // alternate as between separate launches), its status words the other area
-            ++pi;
-            p.status = sw() ? KARG(status2) : KARG(status);
-            tkp = tkp_of();
-            const bool dn = __hip_atomic_load(p.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-            n = uni64(__hip_atomic_load(const_cast<uint64_t*>(sw() ? KARG(total) : KARG(n_dev)), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT));
-            ntiles = (uint32_t)((n + kTileTok - 1) / kTileTok);
-            if (dn || blockIdx.x >= ntiles) break;   // uniform over the grid / per workgroup
-            // the iteration counters start over: the ring words count arrivals per iteration (phase 1
-            // only where an iteration has a tile), so a pass's drain iterations would skew them
-            if (tid == 0) {
-                s_tk0[0] = atomicAdd(tkp, 1u);
-                s_tk0[1] = atomicAdd(tkp, 1u);
-                for (int r = 0; r < kRing; ++r) { s_p1cnt[r] = 0; s_emc[r] = 0; }
-                s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
-            }
-            load_starts();
-            __syncthreads();
-            it = 0;
-            T = uni(s_tk0[0]);
-            Tq = uni(s_tk0[1]);
-            Tp = kNone;
-            Te = kNone;
-            if (T >= ntiles || Tq >= ntiles) Tq = kNone;
-            __syncthreads();
         }
     }
 }
@@ -2988,27 +2641,10 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
 // Measured against it: 16-byte loads writing two 16-byte blocks each, 4 in flight per thread
 // over 65,536 workgroups (0.607 ms); 8-byte blocks with 2 or 4 per thread, or fewer workgroups
 // (0.55-0.62 ms).
-#ifndef BLT_BASIC_VEC
-#define BLT_BASIC_VEC 1
-#endif
-// nt stores (2): 0.512-0.514 -> 0.492-0.494 ms per GiB; nt loads (1, 3) less
-#ifndef BLT_BASIC_NT
-#define BLT_BASIC_NT 2
-#endif
-#ifndef BLT_BASIC_BLOCKS
-#define BLT_BASIC_BLOCKS (1 << 24)
-#endif
-constexpr int kBasicVec = BLT_BASIC_VEC;
+// nt stores: 0.512-0.514 -> 0.492-0.494 ms per GiB (nt loads measured slower)
+constexpr uint64_t kBasicMaxBlocks = 1u << 24;
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
-template <typename T> __device__ __forceinline__ T ld_stream(const T* p) {
-    if constexpr ((BLT_BASIC_NT & 1) != 0) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-template <typename T> __device__ __forceinline__ void st_stream(T v, T* p) {
-    if constexpr ((BLT_BASIC_NT & 2) != 0) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 // bytes b0..b7 -> [0, b0, 0, b1, ..., 0, b7]
 __device__ __forceinline__ v4u basic_expand8(v2u w) {
     v4u a;
@@ -3025,14 +2661,7 @@ __global__ __launch_bounds__(256) void basic_expand_kernel(const uint8_t* __rest
     const v2u* src = reinterpret_cast<const v2u*>(in);
     v4u* dst = reinterpret_cast<v4u*>(out);
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (kBasicVec - 1) * stride < n8; i += kBasicVec * stride) {
-        v2u w[kBasicVec];
-#pragma unroll
-        for (int u = 0; u < kBasicVec; ++u) w[u] = ld_stream(src + i + u * stride);
-#pragma unroll
-        for (int u = 0; u < kBasicVec; ++u) st_stream(basic_expand8(w[u]), dst + i + u * stride);
-    }
-    for (; i < n8; i += stride) dst[i] = basic_expand8(src[i]);
+    for (; i < n8; i += stride) __builtin_nontemporal_store(basic_expand8(src[i]), dst + i);
     for (uint64_t k = n8 * 8 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
         out[2 * k] = 0;
         out[2 * k + 1] = in[k];
@@ -3422,27 +3051,6 @@ hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_scan_chain(const PassParams& p, int device, hipStream_t s) {
-    if (p.n == 0) return hipSuccess;
-    if (!p.status2 || !p.pass_ctr || p.npasses == 0 || p.npasses > kChainMaxPasses || p.nchunks > kChainMaxChunks)
-        return hipErrorInvalidValue;
-    const uint64_t ranges = (p.n + kTokRange - 1) / kTokRange;
-    hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
-    const bool lds = p.hbytes <= kHashLdsMax;
-    const int mode = lds ? (p.hone ? 2 : 1) : 0;
-    const void* fn = mode == 2 ? (const void*)seg::scan_tokens_kernel<2, false, true>
-                     : mode == 1 ? (const void*)seg::scan_tokens_kernel<1, false, true>
-                                 : (const void*)seg::scan_tokens_kernel<0, false, true>;
-    const uint32_t ntiles = (uint32_t)((p.n + kTilePosTok - 1) / kTilePosTok);
-    const int grid = grid_for(ntiles, device, fn, seg::kThreads, 11 + mode);
-    const size_t smem = lds ? ((size_t)p.hbytes + 1023) & ~(size_t)1023 : 0;
-    const dim3 g((unsigned)grid), b(seg::kThreads);
-    if (mode == 2) hipLaunchKernelGGL((seg::scan_tokens_kernel<2, false, true>), g, b, smem, s, p);
-    else if (mode == 1) hipLaunchKernelGGL((seg::scan_tokens_kernel<1, false, true>), g, b, smem, s, p);
-    else hipLaunchKernelGGL((seg::scan_tokens_kernel<0, false, true>), g, b, 0, s, p);
-    return hipGetLastError();
-}
-
 hipError_t launch_scan_fused(const PassParams& p, int device, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
     if (p.hbytes > kHashLdsMax || p.cs < kMinChunkBytes || !p.fused_fail) return hipErrorInvalidValue;
@@ -3459,9 +3067,9 @@ hipError_t launch_scan_fused(const PassParams& p, int device, hipStream_t s) {
 
 hipError_t launch_basic_expand(const uint8_t* in, uint64_t n, uint8_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    uint64_t blocks = (n / 8 / kBasicVec + 255) / 256;    // one pass of kBasicVec blocks per thread
+    uint64_t blocks = (n / 8 + 255) / 256;    // one 8-byte block per thread
     if (blocks < 1) blocks = 1;
-    if (blocks > BLT_BASIC_BLOCKS) blocks = BLT_BASIC_BLOCKS;
+    if (blocks > kBasicMaxBlocks) blocks = kBasicMaxBlocks;
     hipLaunchKernelGGL(basic_expand_kernel, dim3((unsigned)blocks), dim3(256), 0, s, in, n, out);
     return hipGetLastError();
 }
@@ -3546,12 +3154,42 @@ __device__ __forceinline__ bool sp_compact_skip(const SparseParams& q, const uin
 // on selfval's ~60 K seeds).  A lane takes 32 aligned positions (64 bytes of tokens, one word of each bitmap,
 // stored whole: the seed bitmap, the holes and the later passes' two seed bitmaps zeroed); the next
 // lane's first token comes by DPP.  The bucket table is staged in LDS when it fits (kLds).
+// The detect gate: block b counts the mergeable pairs among 8192 positions from b n / 64 (chunk
+// starts ignored: an estimate), one atomic per block.
+__global__ __launch_bounds__(256) void sparse_sample_kernel(SparseParams q) {
+    __shared__ uint32_t s_w[4];
+    if (sp_gated(q)) return;
+    const uint64_t n = *q.n_dev;
+    const uint64_t p0 = n <= kSparseSample ? (uint64_t)blockIdx.x * 8192u
+                                           : (n - 8192u) / (kSparseSampleBlocks - 1u) * blockIdx.x;
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < 32; ++k) {
+        const uint64_t i = p0 + 32ull * threadIdx.x + k;
+        if (i + 1 < n) cnt += sp_lookup(q, sp_key(q, i, i + 1)) >> 31;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (t) atomicAdd(q.sample, t);
+    }
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     if (sp_gated(qa)) return;
     SparseParams q = qa;
     q.n = *qa.n_dev;
+    if (q.sample) {   // the gate: more seeds predicted than half the lists hold, not taken
+        const uint64_t sampled = q.n < kSparseSample ? q.n : kSparseSample;
+        if ((uint64_t)*q.sample * q.n > (uint64_t)(q.cap / 2) * sampled) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(q.flags, 3u);
+            return;
+        }
+    }
     const int lane = threadIdx.x & 63;
     const uint2* tab = q.hbuckets;
     if constexpr (kLds) {
@@ -3637,7 +3275,7 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
 __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_base, s_run;
-    if (sp_gated(qa)) return;
+    if (sp_gated(qa) || (*qa.flags & 2u)) return;   // (the detect gate: not taken)
     SparseParams q = qa;
     q.n = *qa.n_dev;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -4057,6 +3695,7 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
     const bool lds = q.hbytes && q.hbytes <= kHashLdsMax;
     if (blocks > 2048 && !(lds && q.hbytes <= 4096)) blocks = 2048;
     if (blocks < 1) blocks = 1;
+    if (q.sample) hipLaunchKernelGGL(sparse_sample_kernel, dim3(kSparseSampleBlocks), dim3(256), 0, s, q);
     if (lds)
         hipLaunchKernelGGL(sparse_detect_kernel<true>, dim3((unsigned)blocks), dim3(256), q.hbytes, s, q);
     else

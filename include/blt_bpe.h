@@ -148,6 +148,15 @@ typedef struct blt_run_config {
 
 int blt_run_tokenizer(const blt_run_config *cfg);
 
+/* Logging of run_tokenizer, as the reference binary sets it up (src/main.rs:83-85:
+ * tracing_subscriber::fmt with the RUST_LOG env filter): reads RUST_LOG (BLT_LOG when RUST_LOG is
+ * unset) once; without either only errors are logged.  Lines go to stdout, as tracing's fmt
+ * subscriber writes them: "<UTC time>  LEVEL <target>: <message> <field>=<value>".  Messages and
+ * levels follow the reference: lib.rs:247, :251, :265, :273-279 (info), pipeline.rs:63, :203 (info),
+ * pipeline.rs:108, :315, :323, :401 (debug, per chunk), pipeline.rs:409 (error), tokenizer.rs:113
+ * (debug).  A library user that does not call it (the Python binding, as blt_python) logs nothing. */
+void blt_log_init_from_env(void);
+
 /* ---------------------------------------------------------------------------------------
  * Device-resident entry points (inputs already in HBM on the current HIP device).
  * ------------------------------------------------------------------------------------- */

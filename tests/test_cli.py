@@ -4,6 +4,7 @@ and add chunked parity against the C oracle; the CPU cases cover argument handli
 (no tokenising) and the loud failure without a GPU.
 """
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -146,8 +147,14 @@ def test_stdout_appended_and_shared(tmp_path):
 
 @pytest.mark.skipif(_gpu_present(), reason="checks the no-GPU failure")
 def test_tokenising_without_gpu_fails_loudly():
-    r = run([], b"hello")
-    assert r.returncode == 1 and b"Error running tokenizer" in r.stderr and r.stdout == b""
+    env = {k: v for k, v in os.environ.items() if k not in ("RUST_LOG", "BLT_LOG")}
+    r = run([], b"hello", env=env)
+    assert r.returncode == 1 and b"Error running tokenizer" in r.stderr
+    # stdout holds no token, only the pipeline's error event (pipeline.rs:409; errors are logged by
+    # default and tracing's fmt subscriber writes to stdout)
+    lines = _log_lines(r.stdout)
+    assert len(lines) == 1 and lines[0][0] == "ERROR" and lines[0][3].startswith("Error in processed chunk:")
+    assert r.stdout.count(b"\n") == 1
 
 
 # ---- GPU: the reference's CLI tests, then chunked parity ----------------------------------
@@ -272,3 +279,45 @@ def test_cli_stdin_reads_at_most_2mib(tmp_path):
     arr = np.frombuffer(data, np.uint8)
     assert r.stdout == O.COracle({(97, 97): 256}).run(arr, 2 << 20, threads=4).tobytes()
     assert r.stdout != O.COracle({(97, 97): 256}).run(arr, 16 << 20, threads=4).tobytes()
+
+
+# ---- logging (the reference's tracing subscriber, src/main.rs:83-85; RUST_LOG) -------------------
+LOG_RE = re.compile(r"^\d{4}-\d\d-\d\dT\d\d:\d\d:\d\d\.\d{6}Z (ERROR| WARN| INFO|DEBUG|TRACE) (\S.*?): (blt_core[:\w]*): (.*)$")
+
+
+def _log_lines(out: bytes):
+    return [m.groups() for m in (LOG_RE.match(line) for line in out.decode("latin-1").splitlines()) if m]
+
+
+def test_log_levels_and_messages(tmp_path):
+    """RUST_LOG=info: the reference's info events in its order (lib.rs:247, :273-279, :251,
+    pipeline.rs:63, lib.rs:265), on stdout (tracing's fmt writer); debug adds one line per chunk
+    (pipeline.rs:108); no RUST_LOG: nothing but errors.  Passthrough needs no GPU."""
+    src, dst = tmp_path / "in.bin", tmp_path / "out.bin"
+    src.write_bytes(os.urandom(600_000))
+    args = ["--passthrough", "-i", str(src), "-o", str(dst), "--chunksize", "256KB"]
+    r = run(args, env=dict(os.environ, RUST_LOG="info"))
+    assert r.returncode == 0, r.stderr
+    lines = _log_lines(r.stdout)
+    assert [(lv.strip(), msg) for lv, _, _, msg in lines] == [
+        ("INFO", "Starting tokenizer"),
+        ("INFO", "Using passthrough strategy (file copying without tokenization)."),
+        ("INFO", "Chunk size determined effective_chunk_size=262144"),
+        ("INFO", "Running pipeline in Mmap mode for file of size: 600000"),
+        ("INFO", "Tokenizer run completed successfully")]
+    assert lines[0][1] == 'run_tokenizer{input=Some("%s") output=Some("%s")}' % (src, dst)
+    assert dst.read_bytes() == src.read_bytes()
+    r = run(args, env=dict(os.environ, RUST_LOG="blt_core=debug"))
+    dbg = [msg for lv, _, tgt, msg in _log_lines(r.stdout) if lv == "DEBUG"]
+    assert dbg == ["Received result for mmap task task_id=%d" % k for k in range(3)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RUST_LOG", "BLT_LOG")}
+    r = run(args, env=env)
+    assert r.returncode == 0 and r.stdout == b""
+    r = run(args, env=dict(env, BLT_LOG="warn"))
+    assert r.stdout == b""
+    r = run(["--passthrough", "--chunksize", "256KB"], stdin=b"abc", env=dict(env, RUST_LOG="debug"))
+    msgs = [msg for _, _, _, msg in _log_lines(r.stdout)]
+    assert "Running pipeline in Stream mode for stdin" in msgs
+    assert "Spawning chunk processing task task_id=0 bytes=3" in msgs
+    assert "Input stream reached EOF" in msgs
+    assert r.stdout.endswith(b"abc") or b"abc" in r.stdout

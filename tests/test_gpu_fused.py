@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _fused_before_sparse():
-    """The fused kernel's tests keep it for cyclic maps too: sparse policy 2 (the fused passes, then
-    the sparse ones) instead of the default 4 (the byte pass, then the sparse ones)."""
-    prev = _lib.lib().blt_debug_set_sparse(2)
+def _fused_for_cyclic_maps():
+    """The fused kernel's tests keep it for cyclic maps too: the sparse passes off (by default a
+    cyclic map takes the byte pass and then the sparse passes, no fused kernel)."""
+    prev = _lib.lib().blt_debug_set_sparse(0)
     yield
     _lib.lib().blt_debug_set_sparse(prev)
 

@@ -17,10 +17,26 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
            UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
 
 
+_BUILT = []
+
+
 def _driver():
-    if not os.path.exists(DRIVER):
-        subprocess.run(["make", "-C", ROOT, "-j8", "sanitize"], check=True, capture_output=True)
+    """`make sanitize` once per session, every session: make rebuilds the driver whenever a source
+    it is built from changed (round 4 only built it when absent, and a stale driver reported false
+    device failures after the library's host code changed)."""
+    if not _BUILT:
+        r = subprocess.run(["make", "-C", ROOT, "-j8", "sanitize"], capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        _BUILT.append(True)
     return DRIVER
+
+
+def test_sanitize_driver_rebuilt_when_stale():
+    """The driver is up to date with the library's host sources after _driver() (make -q: nothing
+    left to rebuild)."""
+    _driver()
+    r = subprocess.run(["make", "-C", ROOT, "-q", "sanitize"], capture_output=True)
+    assert r.returncode == 0
 
 
 def test_host_checks_under_asan_ubsan():

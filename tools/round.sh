@@ -78,7 +78,7 @@ for st in "$@"; do
         --workload "$a" > "$O/prof_$a.log" 2>&1)
       find "$O/prof_$a" -name '*kernel_stats.csv' -exec head -4 {} \; | cut -c1-160 ;;
     proff2)
-      # proff2[:ROWS[:ENV]]  (ENV: NAME=VALUE for the profiled run, e.g. BLT_CHAIN=0)
+      # proff2[:ROWS[:ENV]]  (ENV: NAME=VALUE for the profiled run)
       rows=${a:-multi,wrap,selfval,chain}
       pd=prof_f2${a:+_${a//,/_}}${b:+_${b//=/}}
       (cd /tmp && export TMPDIR=/tmp && { [ -z "$b" ] || export "$b"; } && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
