@@ -515,6 +515,7 @@ def main():
     cpu = None
     cpu_opt = None
     exact = None
+    exp = None
     usable, affinity, ncpu = usable_cores()
     threads = max(1, args.cpu_threads or usable)
     extras = {}
@@ -553,13 +554,18 @@ def main():
                                  f"pass per chunk (single-pass map), {threads} threads", "seconds": round(fast_s, 3),
                        "matches_port": bool(np.array_equal(fast, exp))}
         del fast
-        if not args.no_extra and wl == "cfg3":
-            del d_in, d_out, ws
-            only = tuple(x for x in args.only_configs.split(",") if x)
-            extras["configs"] = extra_configs(blt_amd, synth, O, threads, only)
-            if not only:
-                extras["end_to_end"], extras["per_chunk_path"] = host_paths(blt_amd, strategy, host, exp)
-                extras["cli_end_to_end"] = cli_end_to_end(synth, host, merges, exp)
+    if rank == 0 and not distributed and not args.no_extra and wl == "cfg3":
+        # the other configs (kernel-only rates) and the host paths; --only-configs runs a subset, also
+        # without the CPU baseline (every row still checks its output against the oracle)
+        from oracle import oracle as O
+        del d_in, d_out, ws
+        only = tuple(x for x in args.only_configs.split(",") if x)
+        extras["configs"] = extra_configs(blt_amd, synth, O, threads, only)
+        if not only:
+            if exp is None:
+                exp = O.COracle(merges).run(host, CHUNK, threads=threads)
+            extras["end_to_end"], extras["per_chunk_path"] = host_paths(blt_amd, strategy, host, exp)
+            extras["cli_end_to_end"] = cli_end_to_end(synth, host, merges, exp)
 
     if rank == 0:
         strong = wl in STRONG_TOTAL

@@ -636,7 +636,7 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
         L.sp_tileo = L.sp_merges + up16(12 * cap);
         L.sp_status = L.sp_tileo + up16(4 * ((sptiles + 15) & ~15ull) + 16);
         L.sp_ctr = L.sp_status + up16(8 * sptiles);
-        L.bytes = L.sp_ctr + 4ull * kSparseCtrWords;
+        L.bytes = L.sp_ctr + up16(4ull * kSparseCtrWords);   // (whole 16-byte units: one fill kernel)
     }
     return L;
 }
@@ -815,7 +815,8 @@ int chain_sticky(const blt_bpe* h, uint8_t* ws, const WsLayout& L, uint64_t pass
 
 // Sparse passes of a cyclic map (blt::launch_sparse_*; bpe_kernels.hip explains why they are the
 // greedy passes), tried once per encode: enqueued right behind the byte pass (no fused kernel) for
-// maps whose byte pass cannot end the chain, at the first read of the pass counts for the others.
+// maps whose byte pass cannot end the chain, else at the first read of the pass counts whose last
+// pass merged under 1/16 of its tokens.
 // On selfval (256 MiB): 0.85 ms against 1.01 behind the fused passes 1 + 2 and 1.34 with full
 // passes only: the byte pass and one more sparse pass (u16 pass 1's ~60 K merges) cost less than
 // the fused kernel.  Test hook blt_debug_set_sparse(0) turns them off (full passes only, the fused
@@ -883,7 +884,8 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
     (void)dev;
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
-    HIP_TRY(hipMemsetAsync(ws + L.sp_tileo, 0, (L.sp_ctr - L.sp_tileo) + 4ull * kSparseCtrWords, s));
+    // a size in whole 16-byte units: the runtime splits any other into two fill kernels (~5 us each)
+    HIP_TRY(hipMemsetAsync(ws + L.sp_tileo, 0, (L.sp_ctr - L.sp_tileo) + up16(4ull * kSparseCtrWords), s));
     blt::SparseParams q{};
     q.tok = reinterpret_cast<uint16_t*>(d_out);
     q.n = n_max;
@@ -1138,7 +1140,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         *out_tokens = rec[3];
         return 0;
     }
-    // sparse passes: tried once, right behind the byte pass or at the first read of the pass counts
+    // sparse passes: tried once, right behind the byte pass or at a read of the pass counts
     bool sp_tried = !sp_on;
     t_last_sparse = 0;
     // Before pass k the chain's arrays follow k: its input total is tot[(k - 1) & 1] and it writes
@@ -1203,8 +1205,10 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if ((uint32_t)rec[2]) break;
         if (k - k_idle > n + 8)
             return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)(k - k_idle));
-        const uint64_t N = rec[(k - 1) & 1];   // the tokens the last pass left
-        if (!sp_tried) {
+        // the last pass k - 1 left N tokens out of Nin (Nin unknown after the fused passes): the sparse
+        // passes are tried once that pass merged under 1/16 of its tokens
+        const uint64_t N = rec[(k - 1) & 1], Nin = (k >= 3 || !fused) ? rec[k & 1] : 0;
+        if (!sp_tried && Nin >= N && (Nin - N) * 16 < N) {
             sp_tried = true;
             SparseRun r;
             if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), N, nullptr, k, off[cur],

@@ -150,7 +150,7 @@ struct SparseParams {
     uint32_t* sample;           // detect's gate: mergeable pairs among kSparseSample sampled positions
                                 // (zeroed; null: no gate)
 };
-constexpr uint64_t kSparseTile = 16384;   // positions per compaction tile
+constexpr uint64_t kSparseTile = 8192;    // positions per compaction tile
 // Positions the detect gate samples: kSparseSampleBlocks evenly spaced runs of 8192 positions.
 constexpr uint32_t kSparseSampleBlocks = 64;
 constexpr uint32_t kSparseSample = kSparseSampleBlocks * 8192u;

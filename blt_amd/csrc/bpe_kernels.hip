@@ -3156,30 +3156,54 @@ __device__ __forceinline__ bool sp_compact_skip(const SparseParams& q, const uin
 // lane's first token comes by DPP.  The bucket table is staged in LDS when it fits (kLds).
 // The detect gate: block b counts the mergeable pairs among 8192 positions from b n / 64 (chunk
 // starts ignored: an estimate), one atomic per block.
-__global__ __launch_bounds__(256) void sparse_sample_kernel(SparseParams q) {
-    __shared__ uint32_t s_w[4];
+__global__ __launch_bounds__(1024) void sparse_sample_kernel(SparseParams q) {
+    __shared__ uint32_t s_w[16];
     if (sp_gated(q)) return;
     const uint64_t n = *q.n_dev;
+    // 8 positions per thread: one 16-byte load and 8 independent lookups (a loop of dependent
+    // lookups per thread took 9.5 us)
     const uint64_t p0 = n <= kSparseSample ? (uint64_t)blockIdx.x * 8192u
-                                           : (n - 8192u) / (kSparseSampleBlocks - 1u) * blockIdx.x;
-    uint32_t cnt = 0;
-    for (uint32_t k = 0; k < 32; ++k) {
-        const uint64_t i = p0 + 32ull * threadIdx.x + k;
-        if (i + 1 < n) cnt += sp_lookup(q, sp_key(q, i, i + 1)) >> 31;
+                                           : ((n - 8192u) / (kSparseSampleBlocks - 1u) * blockIdx.x) & ~7ull;
+    const uint64_t i0 = p0 + 8ull * threadIdx.x;
+    uint32_t t[9];
+    if (i0 + 9 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(q.tok + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        t[8] = q.tok[i0 + 8];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) t[k] = i0 + k < n ? q.tok[i0 + k] : 0u;
     }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (i0 + k + 1 < n) cnt += sp_lookup(q, t[k] | (t[k + 1] << 16)) >> 31;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, d, 64);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = cnt;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        if (t) atomicAdd(q.sample, t);
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) tot += s_w[k];
+        if (tot) atomicAdd(q.sample, tot);
     }
+}
+
+// Bitmap words per workgroup of sparse_list_kernel (whole rounds of 4096, at most kListBlocks
+// workgroups); the detect kernel counts each one's seeds.
+constexpr uint32_t kListWords = 16 * 256, kListBlocks = 2048;
+__host__ __device__ __forceinline__ uint64_t sp_list_words(uint64_t nwords) {   // bitmap words per workgroup
+    const uint64_t r = (nwords + (uint64_t)kListBlocks * kListWords - 1) / ((uint64_t)kListBlocks * kListWords);
+    return (r ? r : 1ull) * kListWords;
 }
 
 template <bool kLds>
 __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    __shared__ uint32_t s_cnt[4];
     if (sp_gated(qa)) return;
     SparseParams q = qa;
     q.n = *qa.n_dev;
@@ -3209,111 +3233,143 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
         }
         return v;
     };
-    const uint64_t nwords = (q.n + 31) / 32;
+    // 256 words per workgroup and round (block-uniform: one count per round); the round's words
+    // lie in one list workgroup's range (sparse_list_kernel), whose seed count it adds to
+    const uint64_t nwords = (q.n + 31) / 32, lw = sp_list_words(nwords);
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256u + (uint64_t)(threadIdx.x & ~63u); base < nwords; base += stride) {
-        const uint64_t wd = base + (uint64_t)lane;   // the loop is wave-uniform; lanes past the end add nothing
-        const uint64_t i0 = wd * 32;
-        uint32_t w[16];
-        if (i0 + 32 <= q.n) {
-            const uint4* src = reinterpret_cast<const uint4*>(q.tok + i0);
+    for (uint64_t b0 = (uint64_t)blockIdx.x * 256u; b0 < nwords; b0 += stride) {
+        uint32_t nseed = 0;   // this lane's seeds
+        const uint64_t base = b0 + (uint64_t)(threadIdx.x & ~63u);
+        if (base < nwords) {   // (wave-uniform)
+            const uint64_t wd = base + (uint64_t)lane;   // lanes past the end add nothing
+            const uint64_t i0 = wd * 32;
+            uint32_t w[16];
+            if (i0 + 32 <= q.n) {
+                const uint4* src = reinterpret_cast<const uint4*>(q.tok + i0);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint4 v = src[k];
-                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-            }
-        } else {
+                for (int k = 0; k < 4; ++k) {
+                    const uint4 v = src[k];
+                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+                }
+            } else {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t lo = i0 + 2u * k < q.n ? q.tok[i0 + 2u * k] : 0u;
-                const uint32_t hi = i0 + 2u * k + 1u < q.n ? q.tok[i0 + 2u * k + 1u] : 0u;
-                w[k] = lo | (hi << 16);
+                for (int k = 0; k < 16; ++k) {
+                    const uint32_t lo = i0 + 2u * k < q.n ? q.tok[i0 + 2u * k] : 0u;
+                    const uint32_t hi = i0 + 2u * k + 1u < q.n ? q.tok[i0 + 2u * k + 1u] : 0u;
+                    w[k] = lo | (hi << 16);
+                }
             }
-        }
-        // the chunk starts in the wave's 2048 positions and the one after (wave-uniform: a binary
-        // search over the sorted chunk starts, then the few in range): this lane's chunk-start
-        // bits, and whether position i0 + 32 starts a chunk
-        const uint64_t W0 = base * 32;
-        uint64_t lo = 0, hi = q.nchunks;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (q.coff_in[mid] < W0) lo = mid + 1;
-            else hi = mid;
-        }
-        uint32_t csw = 0, nc = 0;
-        for (uint64_t c = lo; c < q.nchunks; ++c) {
-            const uint64_t p = q.coff_in[c];
-            if (p > W0 + 2048) break;
-            if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
-            nc |= p == i0 + 32 ? 1u : 0u;
-        }
-        // lane + 1's first token (wave_shl:1); lane 63 reads it
-        uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
-        if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
-        if (wd < nwords) {
-            uint32_t mask = 0;
-            const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
+            // the chunk starts in the wave's 2048 positions and the one after (wave-uniform: a binary
+            // search over the sorted chunk starts, then the few in range): this lane's chunk-start
+            // bits, and whether position i0 + 32 starts a chunk
+            const uint64_t W0 = base * 32;
+            uint64_t lo = 0, hi = q.nchunks;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (q.coff_in[mid] < W0) lo = mid + 1;
+                else hi = mid;
+            }
+            uint32_t csw = 0, nc = 0;
+            for (uint64_t c = lo; c < q.nchunks; ++c) {
+                const uint64_t p = q.coff_in[c];
+                if (p > W0 + 2048) break;
+                if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
+                nc |= p == i0 + 32 ? 1u : 0u;
+            }
+            // lane + 1's first token (wave_shl:1); lane 63 reads it
+            uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
+            if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
+            if (wd < nwords) {
+                uint32_t mask = 0;
+                const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
 #pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                const uint32_t a = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
-                if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
+                for (int k = 0; k < 32; ++k) {
+                    const uint32_t a = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
+                    if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
+                }
+                q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
+                q.bits_out[wd] = 0u;
+                q.bits_alt[wd] = 0u;
+                q.holes[wd] = 0u;
+                nseed = (uint32_t)__popc(mask);
             }
-            q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
-            q.bits_out[wd] = 0u;
-            q.bits_alt[wd] = 0u;
-            q.holes[wd] = 0u;
         }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) nseed += (uint32_t)__shfl_xor((int)nseed, d, 64);
+        if (lane == 0) s_cnt[threadIdx.x >> 6] = nseed;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+            if (c) atomicAdd(reinterpret_cast<unsigned long long*>(q.status + b0 / lw), (unsigned long long)c);
+        }
+        __syncthreads();   // (s_cnt read)
     }
 }
 
-// The first pass's seed list from the detect kernel's bitmap: a workgroup per contiguous range of
-// words counts its seeds, reserves its part of the list with one atomic, then writes the seeds in
-// position order, 256 words at a time (a workgroup scan per round).  A first pass that reads its
-// bitmap directly, a lane per word, measured 549 us on selfval against 20 us from this list (a lane
-// walks its word's seeds one after another, and a long run's seeds sit in few words).
+// The first pass's seed list from the detect kernel's bitmap.  A workgroup per kListBlocks-th of
+// the bitmap (whole rounds of 4096 words; 16 consecutive words per thread and round, four 16-byte
+// loads); the detect kernel added each round's seeds to the count of the list workgroup whose
+// words they are (one atomic per 256 words), so a workgroup's place in the list is the sum of the
+// counts before it, read at once (at most kListBlocks words), and its seeds go out in position
+// order with one workgroup scan per round.  (A first pass that reads its bitmap directly, a lane per
+// word, measured 549 us on selfval against 20 us from this list: a lane walks its word's seeds one
+// after another, and a long run's seeds sit in few words.  Lists with one atomic per workgroup on
+// the list's counter: 31-45 us, the atomics serialised (~11 ns each on one word:
+// tools/atomic_probe.hip); with a look-back over the workgroups, all resident at once: 18.5 us; counts added by detect's
+// waves, one atomic each: list 11 us, detect +20 us.)
+// The counts are the compaction's status words (zeroed with the run's counters), which the move
+// kernel later marks with another bit.
 __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
-    __shared__ uint32_t s_base, s_run;
+    __shared__ uint32_t s_pre[4];
     if (sp_gated(qa) || (*qa.flags & 2u)) return;   // (the detect gate: not taken)
-    SparseParams q = qa;
-    q.n = *qa.n_dev;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t nwords = (q.n + 31) / 32;
-    const uint64_t per = ((nwords + gridDim.x - 1) / gridDim.x + 255) & ~255ull;
-    const uint64_t w0 = (uint64_t)blockIdx.x * per, w1 = w0 + per < nwords ? w0 + per : nwords;
-    if (w0 >= w1) return;   // (uniform)
-    uint32_t h = 0;
-    for (uint64_t wd = w0 + tid; wd < w1; wd += 256) h += (uint32_t)__popc(q.bits_in[wd]);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
+    const uint64_t nwords = (*qa.n_dev + 31) / 32, per = sp_list_words(nwords);
+    const uint64_t wb0 = (uint64_t)b * per, wb1 = wb0 + per < nwords ? wb0 + per : nwords;
+    if (wb0 >= nwords) return;   // (uniform)
+    uint32_t pre = 0;   // seeds of the workgroups before this one
+    for (uint32_t k = tid; k < b; k += 256) pre += (uint32_t)qa.status[k];
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) h += (uint32_t)__shfl_xor((int)h, d, 64);
-    if (lane == 0) s_w[wave] = h;
-    __syncthreads();
-    if (tid == 0) {
-        const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-        s_base = tot ? atomicAdd(q.nseeds_out, tot) : 0u;
-        s_run = 0u;
-    }
-    __syncthreads();
-    const uint32_t base = s_base;
-    for (uint64_t r0 = w0; r0 < w1; r0 += 256) {   // (uniform)
-        const uint64_t wd = r0 + tid;
-        const uint32_t m = wd < w1 ? q.bits_in[wd] : 0u;
-        const uint32_t c = (uint32_t)__popc(m);
+    for (int d = 32; d >= 1; d >>= 1) pre += (uint32_t)__shfl_xor((int)pre, d, 64);
+    if (lane == 0) s_pre[wave] = pre;
+    uint32_t base = 0;   // (set after the first barrier)
+    for (uint64_t r0 = wb0; r0 < wb1; r0 += kListWords) {   // (uniform)
+        const uint64_t w0 = r0 + 16ull * tid;
+        uint32_t m[16];
+        if (w0 + 16 <= wb1) {   // (the bitmaps are 16-byte aligned)
+            const uint4* src = reinterpret_cast<const uint4*>(qa.bits_in + w0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = src[k];
+                m[4 * k] = v.x; m[4 * k + 1] = v.y; m[4 * k + 2] = v.z; m[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) m[k] = w0 + k < wb1 ? qa.bits_in[w0 + k] : 0u;
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) c += (uint32_t)__popc(m[k]);
         const uint32_t incl = wave_incl_scan(c, (int)lane);
-        __syncthreads();   // (s_w, s_run of the round before read)
         if (lane == 63) s_w[wave] = incl;
         __syncthreads();
-        uint32_t o = base + s_run + incl - c;
+        if (r0 == wb0) base = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+        uint32_t o = base + incl - c;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) o += k < wave ? s_w[k] : 0u;
-        for (uint32_t mm = m; mm; mm &= mm - 1u, ++o) {
-            if (o < q.cap) q.seeds_out[o] = (uint32_t)(32ull * wd + (uint64_t)__builtin_ctz(mm));
-            else atomicOr(q.flags, 3u);
+        base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (c) {
+            for (int k = 0; k < 16; ++k) {
+                for (uint32_t mm = m[k]; mm; mm &= mm - 1u, ++o) {
+                    if (o < qa.cap) qa.seeds_out[o] = (uint32_t)(32ull * (w0 + k) + (uint64_t)__builtin_ctz(mm));
+                    else atomicOr(qa.flags, 3u);
+                }
+            }
         }
-        __syncthreads();
-        if (tid == 0) s_run += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();   // (s_w read)
     }
+    if (wb1 == nwords && tid == 0) *qa.nseeds_out = base;   // the last workgroup: the list's length
 }
 
 // One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.  The first pass
@@ -3443,16 +3499,20 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
     }
 }
 
-// Compaction of the hole layout in place.  The apply kernels counted the holes per tile of 16384
+// Compaction of the hole layout in place.  The apply kernels counted the holes per tile of 8192
 // positions; one workgroup scans the counts (a tile's output position is its first position less the
-// holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per tile from a ticket
-// (16384 positions: 8-token groups, four per thread, consecutive lanes on consecutive groups) loads its
-// input, stages its tokens in LDS, marks its input read, waits until every earlier tile whose input
-// its output range overlaps has marked its own (the output of tile T lies in [0, end of T's input):
-// the one or two tiles its range falls in), and writes the range with 16-byte
-// stores (2-byte ones at the two partial ends, which the neighbouring tiles share).  Persistent
-// workgroups take tiles from a ticket.
-constexpr int kCpThreads = 512;
+// holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per tile,
+// in blockIdx order (8192 positions: 8-token groups, four per thread, consecutive lanes on
+// consecutive groups), loads its input, stages its tokens in LDS, marks its input read, waits until
+// every earlier tile whose input its output range overlaps has marked its own (the output of tile T
+// lies in [0, end of T's input): the one or two tiles its range falls in), and writes the range with
+// 16-byte stores (2-byte ones at the two partial ends, which the neighbouring tiles share).  Small
+// workgroups, many per CU (eight waves per SIMD): the loads of the tiles in flight hide each other's
+// latency.  Tiles in blockIdx order, not from a ticket (one atomic per tile on one word: 399 us on
+// selfval against ~10 ns per ticket): every XCD dispatches its workgroups in order, so the lowest
+// unfinished tile is running and waits for nobody, and a wait on a lower tile always ends.
+constexpr int kCpThreads = 256;
+constexpr uint64_t kMvRead = 1ull << 61;   // a tile's input is read (the list kernel's counts stay below it)
 static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
 
 // The tiles' hole counts turned in place into the holes before each tile, and the total into
@@ -3515,145 +3575,107 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
     if (tid == 0) *q.super_cnt = s_carry;
 }
 
-__global__ __launch_bounds__(kCpThreads) void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
-    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile];
+__global__ __launch_bounds__(kCpThreads) __attribute__((amdgpu_waves_per_eu(8)))
+void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
+    // staged tokens, shifted by the output's offset in its 8-token group so that every output group
+    // is one aligned 16-byte LDS word
+    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile + 8];
     __shared__ uint32_t s_wsum[4][kCpThreads / 64];
-    __shared__ uint32_t s_T[2];
     if (sp_compact_skip(qa, nseeds0)) return;
-    SparseParams q = qa;
-    q.n = *qa.n_dev;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
-    // level j: 8-token group G = j * kCpThreads + tid (consecutive lanes read consecutive 16 bytes)
+    const uint64_t n = *qa.n_dev, ntiles = (n + kSparseTile - 1) / kSparseTile, T = blockIdx.x;
+    if (T >= ntiles) return;   // (uniform: the grid is sized for the host's count, >= the device's)
+    const uint64_t tile0 = T * kSparseTile;
+    const uint32_t hb = qa.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
+    const uint32_t hnext = T + 1 < ntiles ? qa.tile_cnt[T + 1] : *qa.super_cnt;
+    // level j: 8-token group G = j * kCpThreads + tid
     uint32_t w[4][4], valid[4];
-    auto load_tile = [&](uint64_t TT) {
-        const uint64_t t0 = TT * kSparseTile;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
-            const uint64_t p = t0 + 8ull * G;
-            valid[j] = 0u;
-            w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
-            if (p < q.n) {
-                const uint64_t left = q.n - p;
-                valid[j] = ~(q.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
-                if (left >= 8) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(q.tok + p);
-                    w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
-                } else {
-                    for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)q.tok[p + k] << (16u * (k & 1u));
-                }
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
+        const uint64_t p = tile0 + 8ull * G;
+        valid[j] = 0u;
+        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
+        if (p < n) {
+            const uint64_t left = n - p;
+            valid[j] = ~(qa.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
+            if (left >= 8) {
+                const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(qa.tok + p));
+                w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
+            } else {
+                for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)qa.tok[p + k] << (16u * (k & 1u));
             }
         }
-    };
-    if (tid == 0) s_T[0] = atomicAdd(q.ticket, 1u);
+    }
+    const uint64_t O = tile0 - hb;
+    const uint32_t e = (uint32_t)(O & 7u);
+    uint32_t cnt[4], incl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        cnt[j] = __popc(valid[j]);
+        incl[j] = wave_incl_scan(cnt[j], lane);
+        if (lane == 63) s_wsum[j][wave] = incl[j];
+    }
     __syncthreads();
-    uint64_t T = s_T[0];
-    if (T < ntiles) load_tile(T);
-    bool first = true;
-    // Persistent, software-pipelined: the next tile's ticket is taken and its input loaded while this
-    // one is staged and written, and it is marked read as soon as its loads are done.  A claimed tile
-    // is loaded by a workgroup that waits only for lower tiles' reads, so the lowest tile in
-    // progress never waits for an unread one.
-    for (uint32_t it = 1; T < ntiles; ++it) {
-        if (tid == 0) s_T[it & 1] = atomicAdd(q.ticket, 1u);
-        const uint64_t tile0 = T * kSparseTile;
-        const uint32_t hb = q.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
-        const uint32_t hnext = T + 1 < ntiles ? q.tile_cnt[T + 1] : *q.super_cnt;
-        const uint64_t O = tile0 - hb;
-        uint32_t cnt[4], incl[4];
+    uint32_t lbase = e;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            cnt[j] = __popc(valid[j]);
-            incl[j] = wave_incl_scan(cnt[j], lane);
-            if (lane == 63) s_wsum[j][wave] = incl[j];
+    for (int j = 0; j < 4; ++j) {
+        uint32_t wb = 0, lt = 0;
+#pragma unroll
+        for (int k = 0; k < kCpThreads / 64; ++k) {
+            const uint32_t v = s_wsum[j][k];
+            wb += k < wave ? v : 0u;
+            lt += v;
         }
-        __syncthreads();
-        uint32_t lbase = 0;
+        uint32_t o = lbase + wb + incl[j] - cnt[j];
+        if (valid[j] == 0xFFu && (o & 1u) == 0u) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
+            d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t wb = 0, lt = 0;
-#pragma unroll
-            for (int k = 0; k < kCpThreads / 64; ++k) {
-                const uint32_t v = s_wsum[j][k];
-                wb += k < wave ? v : 0u;
-                lt += v;
-            }
-            uint32_t o = lbase + wb + incl[j] - cnt[j];
-            if (valid[j] == 0xFFu) {
-                if ((o & 1u) == 0u) {
-                    uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
-                    d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s_out[o + k] = (uint16_t)(w[j][k >> 1] >> (16 * (k & 1)));
-                }
-            } else {
-                for (uint32_t m = valid[j]; m; m &= m - 1u, ++o) {
-                    const uint32_t k = (uint32_t)__builtin_ctz(m);
-                    s_out[o] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
-                }
-            }
-            lbase += lt;
-        }
-        const uint32_t ttot = lbase;
-        const uint64_t in_end = tile0 + kSparseTile < q.n ? tile0 + kSparseTile : q.n;
-        __syncthreads();   // staged; the next ticket visible
-        const uint64_t Tn = s_T[it & 1];
-        if (tid == 0) {
-            if (first) st_publish(q.status + T, 1ull);   // (later tiles were marked when their loads ended)
-            if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(q.ctl, q.sticky, 4u);   // counts vs bitmap
-        }
-        first = false;
-        // else in place already; an output range past the tile's input (bad counts) writes nothing
-        const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
-        if (moves) {
-            if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
-                bool bad = false;
-                const uint64_t ulast = ttot ? (O + ttot - 1) / kSparseTile : 0;
-                const uint64_t uend = ulast + 1 < T ? ulast + 1 : T;
-                for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < uend; u += 64) {
-                    SpinClock clk;
-                    while (st_read(q.status + u) == 0ull) {
-                        if (clk.expired()) { bad = true; break; }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                if (__ballot(bad) != 0ull && lane == 0) flag_error(q.ctl, q.sticky, 1u);
-            }
-            __syncthreads();
-        }
-        if (Tn < ntiles) load_tile(Tn);   // the next tile's loads go out ahead of this tile's stores
-        if (moves) {
-            // tokens [O, O + ttot): 8-token groups g0 .. g1 - 1 whole, the ends token by token
-            const uint64_t e = O + ttot, g0 = (O + 7) / 8, g1 = e / 8;
-            if (g0 < g1) {
-                const uint32_t sh = (uint32_t)(8 * g0 - O);   // s_out index of group g0
-                for (uint64_t g = g0 + (uint64_t)tid; g < g1; g += kCpThreads) {
-                    const uint32_t b = (uint32_t)(8 * (g - g0)) + sh;
-                    uint32_t v[4];
-                    if ((sh & 1u) == 0u) {
-                        const uint32_t* src = reinterpret_cast<const uint32_t*>(s_out) + (b >> 1);
-                        v[0] = src[0]; v[1] = src[1]; v[2] = src[2]; v[3] = src[3];
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) v[k] = (uint32_t)s_out[b + 2 * k] | ((uint32_t)s_out[b + 2 * k + 1] << 16);
-                    }
-                    *reinterpret_cast<uint4*>(q.tok + 8 * g) = make_uint4(v[0], v[1], v[2], v[3]);
-                }
-                const uint64_t head = sh, tail = e - 8 * g1;   // < 8 each
-                if ((uint64_t)tid < head) q.tok[O + tid] = s_out[tid];
-                else if ((uint64_t)tid >= 8 && (uint64_t)tid < 8 + tail) q.tok[8 * g1 + (tid - 8)] = s_out[8 * g1 - O + (tid - 8)];
-            } else {
-                for (uint64_t k = (uint64_t)tid; k < ttot; k += kCpThreads) q.tok[O + k] = s_out[k];
+            for (uint32_t k = 0; k < 8; ++k) {
+                if ((valid[j] >> k) & 1u) s_out[o++] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
             }
         }
-        // the next tile's input is in registers once this wave's loads are done (its stores too: one
-        // counter); after the barrier every wave's are, and the tile is marked read
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();   // (s_out and s_wsum free again)
-        if (tid == 0 && Tn < ntiles) st_publish(q.status + Tn, 1ull);
-        T = Tn;
+        lbase += lt;
+    }
+    const uint32_t ttot = lbase - e;
+    const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
+    __syncthreads();   // staged: every load of the tile done
+    if (tid == 0) {
+        st_publish(qa.status + T, kMvRead);
+        if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(qa.ctl, qa.sticky, 4u);   // counts vs bitmap
+    }
+    // else in place already; an output range past the tile's input (bad counts) writes nothing
+    const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
+    if (!moves) return;   // (uniform)
+    if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
+        bool bad = false;
+        const uint64_t ulast = ttot ? (O + ttot - 1) / kSparseTile : 0;
+        const uint64_t uend = ulast + 1 < T ? ulast + 1 : T;
+        for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < uend; u += 64) {
+            SpinClock clk;
+            while ((st_read(qa.status + u) & kMvRead) == 0ull) {
+                if (clk.expired()) { bad = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (__ballot(bad) != 0ull && lane == 0) flag_error(qa.ctl, qa.sticky, 1u);
+    }
+    __syncthreads();
+    // output groups r = 0 .. nr - 1 (global tokens 8 (O / 8 + r) ..): whole ones with one 16-byte
+    // store, the partial first and last token by token
+    const uint32_t nr = (e + ttot + 7u) / 8u;
+    uint16_t* dst = qa.tok + (O - e);
+    for (uint32_t r = (uint32_t)tid; r < nr; r += kCpThreads) {
+        const uint32_t b = 8u * r;
+        if (b >= e && b + 8u <= e + ttot) {
+            const v4u v = *reinterpret_cast<const v4u*>(s_out + b);
+            __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst + b));
+        } else {
+            for (uint32_t k = b; k < b + 8u; ++k)
+                if (k >= e && k < e + ttot) dst[k] = s_out[k];
+        }
     }
 }
 
@@ -3689,13 +3711,14 @@ static bool sparse_ok(const SparseParams& q) {
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
     // a lane per 32 positions; every position in one wave of workgroups when the table is small
-    // (each workgroup stages it), else a grid of 2048 looping
+    // (each workgroup stages it), else a grid of 2048 looping.  (A workgroup per list workgroup's
+    // words, 16 rounds each, measured 240 us against 142 on selfval.)
     const uint64_t nwords = (q.n + 31) / 32;
     uint64_t blocks = (nwords + 255) / 256;
     const bool lds = q.hbytes && q.hbytes <= kHashLdsMax;
     if (blocks > 2048 && !(lds && q.hbytes <= 4096)) blocks = 2048;
     if (blocks < 1) blocks = 1;
-    if (q.sample) hipLaunchKernelGGL(sparse_sample_kernel, dim3(kSparseSampleBlocks), dim3(256), 0, s, q);
+    if (q.sample) hipLaunchKernelGGL(sparse_sample_kernel, dim3(kSparseSampleBlocks), dim3(1024), 0, s, q);
     if (lds)
         hipLaunchKernelGGL(sparse_detect_kernel<true>, dim3((unsigned)blocks), dim3(256), q.hbytes, s, q);
     else
@@ -3704,9 +3727,9 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
 }
 hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
-    // 2048 workgroups (one atomic each); 8192 measured 99 us against 40 on selfval
-    uint64_t g = ((q.n + 31) / 32 + 255) / 256;
-    if (g > 2048) g = 2048;
+    // the host's count may exceed the device's: extra workgroups return
+    const uint64_t nw = (q.n + 31) / 32, per = sp_list_words(nw);
+    uint64_t g = (nw + per - 1) / per;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(sparse_list_kernel, dim3((unsigned)g), dim3(256), 0, s, q);
     return hipGetLastError();
@@ -3729,9 +3752,7 @@ hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0,
     if (!sparse_ok(q) || !q.total || !nseeds0 || !q.nchunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
     hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(1024), 0, s, q, nseeds0);
-    // persistent: four workgroups per CU (32 KiB of LDS each)
-    const uint64_t grid = ntiles < 1024 ? ntiles : 1024;
-    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)grid), dim3(kCpThreads), 0, s, q, nseeds0);
+    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)ntiles), dim3(kCpThreads), 0, s, q, nseeds0);
     hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q, nseeds0);
     return hipGetLastError();
 }
