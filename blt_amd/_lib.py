@@ -93,6 +93,7 @@ _DEBUG_SIGNATURES = {
     "blt_debug_set_tile_record": (None, [_vp]),
     "blt_debug_last_u16_passes": (ctypes.c_uint32, []),
     "blt_debug_set_shared_contexts": (None, [ctypes.c_int]),
+    "blt_debug_set_pin_ring": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_set_fused": (None, [ctypes.c_int]),
     "blt_debug_last_fused": (ctypes.c_uint32, []),
     "blt_debug_byte_mode": (ctypes.c_int, [_vp]),

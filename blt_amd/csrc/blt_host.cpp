@@ -591,10 +591,10 @@ struct WsLayout {
 constexpr uint32_t kMaxBoundedPasses = 64;
 inline bool chain_bounded(const blt_bpe* h) { return h->chain_depth && h->chain_depth <= kMaxBoundedPasses + 1; }
 // Sparse passes per run_sparse call (one counter pair each, zeroed once; a longer tail goes back to
-// the full passes).  Counter words: [0] overflow flag, [1] compaction ticket, [2 + p] pass p's seeds,
+// the full passes).  Counter words: [0] overflow flag, [1] unused, [2 + p] pass p's seeds,
 // [2 + kSparseMaxPasses + 1 + p] pass p's merges.
 constexpr uint32_t kSparseMaxPasses = 250;
-constexpr uint32_t kSparseCtrWords = 2 + 2 * (kSparseMaxPasses + 1) + 1;   // + the detect gate's sample count
+constexpr uint32_t kSparseCtrWords = 2 + 2 * (kSparseMaxPasses + 1);
 // Chain block of a general map (right after pass 1's status words): u64 pass totals [2], u32 done
 // word, u32 fused-fail word, u64 final total, u32 finish-gate word, pad.
 constexpr uint64_t kChainBlock = 48;
@@ -636,7 +636,7 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
         L.sp_tileo = L.sp_merges + up16(12 * cap);
         L.sp_status = L.sp_tileo + up16(4 * ((sptiles + 15) & ~15ull) + 16);
         L.sp_ctr = L.sp_status + up16(8 * sptiles);
-        L.bytes = L.sp_ctr + up16(4ull * kSparseCtrWords);   // (whole 16-byte units: one fill kernel)
+        L.bytes = L.sp_ctr + up16(4ull * kSparseCtrWords) + 4ull * blt::kSparseSampleBlocks;   // + the gate's sample
     }
     return L;
 }
@@ -884,8 +884,6 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
     (void)dev;
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
-    // a size in whole 16-byte units: the runtime splits any other into two fill kernels (~5 us each)
-    HIP_TRY(hipMemsetAsync(ws + L.sp_tileo, 0, (L.sp_ctr - L.sp_tileo) + up16(4ull * kSparseCtrWords), s));
     blt::SparseParams q{};
     q.tok = reinterpret_cast<uint16_t*>(d_out);
     q.n = n_max;
@@ -908,8 +906,11 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.tile_cnt = reinterpret_cast<uint32_t*>(ws + L.sp_tileo);   // (8 B per tile: the counts padded to 16, the total)
     q.super_cnt = q.tile_cnt + ((L.sp_ntiles + 15) & ~15ull);
     q.status = reinterpret_cast<uint64_t*>(ws + L.sp_status);
-    q.ticket = ctr + 1;
-    q.sample = ctr + (kSparseCtrWords - 1);
+    // counters, tile counts and status words: zeroed by the first sparse kernel (a memset is one
+    // more launch, ~5 us; two when its size is not whole 16-byte units)
+    q.zero = reinterpret_cast<uint4*>(ws + L.sp_tileo);
+    q.zero16 = (uint32_t)(((L.sp_ctr - L.sp_tileo) + up16(4ull * kSparseCtrWords)) / 16);
+    q.sample = reinterpret_cast<uint32_t*>(ws + L.sp_ctr + up16(4ull * kSparseCtrWords));
     q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     q.sticky = h->sticky.load(std::memory_order_acquire);
     uint32_t* seeds[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_seeds0), reinterpret_cast<uint32_t*>(ws + L.sp_seeds1)};
@@ -1243,7 +1244,9 @@ struct PipeSlot {
     uint8_t* d_ws = nullptr;
     uint64_t* d_off = nullptr;
     uint64_t* h_rec = nullptr;        // pinned: [0] tokens, [1..8] control words, [9..] chunk offsets
-    uint64_t win = 0, ws_bytes = 0, nch = 0;
+    uint8_t* h_in = nullptr;          // pinned staging ring (BLT_PIN_RING): the window's bytes,
+    uint8_t* h_out = nullptr;         // and its tokens
+    uint64_t win = 0, ws_bytes = 0, nch = 0, pin = 0;
 };
 #ifndef BLT_PIPE_SLOTS
 #define BLT_PIPE_SLOTS 4
@@ -1339,9 +1342,46 @@ int encode_host_on(const blt_bpe* h, int dev, const uint8_t* in, uint64_t n, uin
     return 0;
 }
 
+// Pinned staging ring of the windowed host path, opt-in: BLT_PIN_RING=1 (or
+// blt_debug_set_pin_ring).  Each slot holds a pinned copy of its window's bytes and tokens; the
+// producer copies the caller's bytes in with kPinCopyThreads threads and the DMA reads pinned memory,
+// the drain copies the tokens out the same way after the device-to-host DMA into pinned memory.  Off
+// by default: the runtime's own path from pageable memory is no slower.
+std::atomic<int> g_pin_ring{-1};   // -1: from the environment at first use
+bool pin_ring_on() {
+    int v = g_pin_ring.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = getenv("BLT_PIN_RING");
+        v = (e && *e && strcmp(e, "0") != 0) ? 1 : 0;
+        g_pin_ring.store(v, std::memory_order_relaxed);
+    }
+    return v != 0;
+}
+#ifndef BLT_PIN_COPY_THREADS
+#define BLT_PIN_COPY_THREADS 4
+#endif
+constexpr int kPinCopyThreads = BLT_PIN_COPY_THREADS;
+// memcpy of n bytes on up to kPinCopyThreads threads (pieces of whole 64 KiB, the caller's thread
+// takes the first)
+void par_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    constexpr uint64_t kMin = 4ull << 20, kAlign = 64ull << 10;
+    const int nt = n < kMin ? 1 : kPinCopyThreads;
+    const uint64_t per = ((n + nt - 1) / nt + kAlign - 1) & ~(kAlign - 1);
+    std::thread th[kPinCopyThreads];
+    for (int t = 1; t < nt; ++t) {
+        const uint64_t a = per * t;
+        if (a >= n) break;
+        th[t] = std::thread([=] { memcpy(dst + a, src + a, std::min(per, n - a)); });
+    }
+    memcpy(dst, src, std::min(per, n));
+    for (int t = 1; t < nt; ++t)
+        if (th[t].joinable()) th[t].join();
+}
+
 // Grows slot P of c for windows of `win` bytes in chunks of cs (device buffers, stream, event,
-// pinned record).  Slots are cached with the context for the process lifetime.
-int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs) {
+// pinned record; the pinned staging ring when `pin`).  Slots are cached with the context for the
+// process lifetime.
+int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs, bool pin = false) {
     const uint64_t nch = (win + cs - 1) / cs;
     const WsLayout L = ws_layout(h, win, cs);
     if (!P.stream) HIP_TRY(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
@@ -1363,6 +1403,15 @@ int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs) {
         P.win = win;
         P.ws_bytes = L.bytes;
         P.nch = nch;
+    }
+    if (pin && P.pin < win) {
+        if (P.h_in) (void)hipHostFree(P.h_in);
+        if (P.h_out) (void)hipHostFree(P.h_out);
+        P.h_in = P.h_out = nullptr;
+        P.pin = 0;
+        HIP_TRY(hipHostMalloc(&P.h_in, up16(win), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&P.h_out, up16(2 * win), hipHostMallocDefault));
+        P.pin = win;
     }
     return 0;
 }
@@ -1401,6 +1450,7 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
     const uint64_t nw = (n + win - 1) / win;
     const uint64_t per_ctx = (nw + g - 1) / g;
     const int slots = (int)std::min<uint64_t>(kPipeSlots, per_ctx);
+    const bool pin = pin_ring_on();
     std::vector<DevCtx*> ctx(g, nullptr);
     struct Release {
         std::vector<DevCtx*>& v;
@@ -1411,7 +1461,7 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
         ctx[d] = ctx_acquire(devs[d]);
         if (!ctx[d]) return fail(BLT_E_IO, "cannot create a HIP stream on device %d", devs[d]);
         for (int k = 0; k < slots; ++k)
-            if (int rc = pipe_slot_ready(h, ctx[d]->pipe[k], std::min(win, n), cs)) return rc;
+            if (int rc = pipe_slot_ready(h, ctx[d]->pipe[k], std::min(win, n), cs, pin)) return rc;
     }
     MultiRun R;
     R.tok.assign(nw, MultiRun::kUnset);
@@ -1433,7 +1483,12 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
             const uint64_t b0 = w * win, len = std::min(win, n - b0);
             const WsLayout L = ws_layout(h, len, cs);
             int rc = 0;
-            if (hipMemcpyAsync(P.d_in, in + b0, len, hipMemcpyHostToDevice, P.stream) != hipSuccess) {
+            const uint8_t* src = in + b0;
+            if (pin) {   // (the slot's pinned copy is free: its window was drained)
+                par_memcpy(P.h_in, src, len);
+                src = P.h_in;
+            }
+            if (hipMemcpyAsync(P.d_in, src, len, hipMemcpyHostToDevice, P.stream) != hipSuccess) {
                 rc = fail(BLT_E_IO, "host-to-device copy failed on device %d", c->device);
             } else if (h->single_pass) {
                 rc = encode_device(h, P.d_in, len, cs, P.d_out, P.d_off, P.d_ws, P.ws_bytes, P.stream, nullptr);
@@ -1458,9 +1513,26 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
             R.cv.notify_all();
         }
     };
+    struct Pending {
+        PipeSlot* P = nullptr;
+        uint64_t o = 0, tok = 0;
+    };
     auto drain = [&](uint64_t d) {
         DevCtx* c = ctx[d];
         if (hipSetDevice(c->device) != hipSuccess) return R.fail_once(fail(BLT_E_IO, "hipSetDevice(%d) failed", c->device));
+        Pending pend;
+        auto finish = [&](Pending& q) {   // (pinned ring) window q's tokens into the output, slot released
+            if (hipStreamSynchronize(q.P->stream) != hipSuccess) {
+                R.fail_once(fail(BLT_E_IO, "device-to-host copy failed on device %d", c->device));
+                return false;
+            }
+            par_memcpy(out + 2 * q.o, q.P->h_out, 2 * q.tok);
+            q.P = nullptr;
+            std::lock_guard<std::mutex> lk(R.mu);
+            ++R.drained[d];
+            R.cv.notify_all();
+            return true;
+        };
         for (uint64_t j = 0, w = d; w < nw; ++j, w += g) {
             {
                 std::unique_lock<std::mutex> lk(R.mu);
@@ -1490,12 +1562,20 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
             }
             if (chunk_off)
                 for (uint64_t k = 1; k <= nch; ++k) (*chunk_off)[k0 + k] = o + P.h_rec[9 + k];
-            if (hipMemcpyAsync(out + 2 * o, P.d_out, 2 * tok, hipMemcpyDeviceToHost, P.stream) != hipSuccess)
+            if (hipMemcpyAsync(pin ? P.h_out : out + 2 * o, P.d_out, 2 * tok, hipMemcpyDeviceToHost, P.stream) != hipSuccess)
                 return R.fail_once(fail(BLT_E_IO, "device-to-host copy failed on device %d", c->device));
+            if (pin) {
+                // the previous window's tokens out of its pinned copy while this one's DMA runs; this
+                // slot is released one window later
+                if (pend.P && !finish(pend)) return;
+                pend = Pending{&P, o, tok};
+                continue;
+            }
             std::lock_guard<std::mutex> lk(R.mu);
             ++R.drained[d];
             R.cv.notify_all();
         }
+        if (pend.P) (void)finish(pend);
     };
     std::vector<std::thread> th;
     th.reserve(2 * g);
@@ -1827,6 +1907,9 @@ uint32_t blt_debug_chain_depth(const blt_bpe* h) { return h ? h->chain_depth : 0
 // contexts even where several share a device (on a one-GPU box: every context's producer and drain
 // threads, sharing the device); 0 restores one context per device.
 void blt_debug_set_shared_contexts(int on) { g_shared_contexts.store(on ? 1 : 0, std::memory_order_relaxed); }
+// Not in the public header: a test hook for the pinned staging ring of the windowed host path
+// (BLT_PIN_RING); returns the previous setting.
+int blt_debug_set_pin_ring(int on) { return g_pin_ring.exchange(on ? 1 : 0) > 0 ? 1 : 0; }
 
 // Test hook: 0 runs every general map on the two-kernel chain, 1 (default) lets eligible maps fuse
 // passes 1 and 2.

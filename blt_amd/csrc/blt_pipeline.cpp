@@ -355,7 +355,8 @@ struct OutMap {
 void map_output(int fd, size_t total, size_t est, OutMap* om);
 
 int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, int fd, size_t head,
-                    const uint8_t* head_bytes, const OutMap& om, const std::string& span) {
+                    const uint8_t* head_bytes, const OutMap& om, std::vector<std::thread>& behind,
+                    const std::string& span) {
     const size_t cap = st.kind == Strategy::kPassthrough ? n : 2 * n;
     const size_t total = head + cap;
     if (total == 0) return 0;
@@ -385,6 +386,8 @@ int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, 
         }
     }
     if (!rc) log_chunks(span, st.kind == Strategy::kBasic, 0, (n + cs - 1) / cs, n, cs);
+    for (auto& t : behind) t.join();   // (populate_behind: done with the mapping too)
+    behind.clear();
     if (om.registered) (void)hipHostUnregister(om.m);
     munmap(om.m, total);
     const std::string msg = rc ? last_error() : std::string();
@@ -448,6 +451,28 @@ void map_output(int fd, size_t total, size_t est, OutMap* om) {
     // (env experiment) the whole mapping page-locked for the runtime's copies
     if (env_on("BLT_OUT_REGISTER", false))
         om->registered = hipHostRegister(om->m, total, hipHostRegisterDefault) == hipSuccess;
+}
+
+// The output's first `est` bytes mapped writable (MADV_POPULATE_WRITE) by `nt` threads in 2 MiB
+// pieces from the start, once the HIP runtime is up and while the tokeniser runs: the device-to-host
+// copies then mostly land in pages that are already mapped, and where they catch up they fault
+// their own.  Done at start-up (map_output, mode 1), the same page-fault storm held the process's
+// mmap lock against the runtime's own start-up (0.11-0.13 -> 0.23 s); behind it, nothing else
+// maps memory.  Best effort: a piece that fails stops that thread.
+void populate_behind(const OutMap& om, size_t est, std::vector<std::thread>& th) {
+    const char* tv = getenv("BLT_OUT_THREADS");
+    const size_t nt = std::max<size_t>(1, std::min<size_t>(16, (tv && *tv) ? (size_t)atoi(tv) : 4));
+    constexpr size_t kPiece = size_t(2) << 20;
+    const size_t len = std::min(est, om.total);
+    const size_t pieces = (len + kPiece - 1) / kPiece;
+    uint8_t* m = om.m;
+    for (size_t t = 0; t < nt; ++t)
+        th.emplace_back([=] {
+            for (size_t i = t; i < pieces; i += nt) {
+                const size_t off = i * kPiece;
+                if (madvise(m + off, std::min(kPiece, len - off), MADV_POPULATE_WRITE) != 0) return;
+            }
+        });
 }
 
 // Stream path (pipeline.rs:196-433): one read per chunk, at most `threads` chunks in flight, a
@@ -747,7 +772,18 @@ int run(const blt_run_config* c) {
     else
         blt_log::emit(blt_log::kInfo, span_pipe.c_str(), "blt_core::pipeline", "Running pipeline in Stream mode for stdin");
     int drc = 1;
-    if (direct) drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om, span_pipe);
+    std::vector<std::thread> behind;
+    struct JoinAll {
+        std::vector<std::thread>& v;
+        ~JoinAll() { for (auto& t : v) if (t.joinable()) t.join(); }
+    } join_behind{behind};
+    if (direct) {
+        // (env: A/B runs) BLT_OUT_BEHIND=0 leaves every page to the copies' own faults
+        const char* pv = getenv("BLT_OUT_POPULATE");
+        if (om.m && !(pv && *pv && atoi(pv) != 0) && env_on("BLT_OUT_BEHIND", true))
+            populate_behind(om, head + (st.kind == Strategy::kBasic ? 2 * n : n), behind);
+        drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om, behind, span_pipe);
+    }
     if (drc <= 0) {
         rc = drc;
     } else {

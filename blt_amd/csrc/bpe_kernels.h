@@ -143,21 +143,24 @@ struct SparseParams {
     uint64_t* total;            // tokens after compaction (may be the word n_dev points to: written last)
     uint32_t* tile_cnt;         // per compaction tile: holes in it (apply kernels), then holes before it (scan)
     uint32_t* super_cnt;        // one word: the holes in all (scan)
-    uint64_t* status;           // per compaction tile: its input is read (zeroed)
-    uint32_t* ticket;           // compaction tile ticket (zeroed)
+    uint64_t* status;           // per compaction tile: the list kernel's seed counts, then the move's
+                                // read marks (zeroed)
     uint32_t* ctl;              // the chain's control block (error flags)
     uint32_t* sticky;
-    uint32_t* sample;           // detect's gate: mergeable pairs among kSparseSample sampled positions
-                                // (zeroed; null: no gate)
+    uint32_t* sample;           // detect's gate: mergeable pairs per sampled block (kSparseSampleBlocks
+                                // words, written whole by the sample kernel)
+    uint4* zero;                // the run's counters, tile counts and status words: zeroed by the
+    uint32_t zero16;            // sample kernel (16-byte units), ahead of every other sparse kernel
 };
 constexpr uint64_t kSparseTile = 8192;    // positions per compaction tile
 // Positions the detect gate samples: kSparseSampleBlocks evenly spaced runs of 8192 positions.
 constexpr uint32_t kSparseSampleBlocks = 64;
 constexpr uint32_t kSparseSample = kSparseSampleBlocks * 8192u;
 // detect: the first pass's seeds (every mergeable pair's first position) into seeds_in / bits_in.
-// With q.sample, a sampling kernel runs first, and detect leaves the run not taken (flags 3, no
-// bitmaps) when the sample predicts more than half the lists' capacity of seeds: a dense cyclic map
-// goes on with the full passes for the cost of a few empty launches.
+// A sampling kernel runs first (it also zeroes the run's counters: no memset), and detect leaves the
+// run not taken (flags 3, no bitmaps) when the sample predicts more than half the lists' capacity of
+// seeds: a dense cyclic map goes on with the full passes for the cost of a few empty launches
+// (ADVICE r4).
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s);
 // the first pass's seed list from the detect kernel's bitmap (q.seeds_out, q.nseeds_out)
 hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s);

@@ -267,6 +267,30 @@ def test_multi_context_many_windows(n_gpus):
     assert np.array_equal(s.process_chunks(data, cs, n_gpus=n_gpus), exp)
 
 
+@pytest.mark.parametrize("n_gpus", [1, 3])
+def test_pinned_staging_ring(n_gpus):
+    """The windowed host path through its pinned staging ring (BLT_PIN_RING; the drain copies a
+    window's tokens out one window behind its DMA): more windows than slots, odd chunks, and a
+    general map (one window per context), bit-exact with the default path and the oracle."""
+    from blt_amd import _lib
+    cs = (1 << 20) + 3
+    n = (200 << 20) + 777
+    data = synth.text(n, seed=78)
+    m = synth.merges_dict(synth.text_merges_50k(synth.text(4 << 20, seed=4), seed=4))
+    s = blt_amd.BpeStrategy(m)
+    g = blt_amd.BpeStrategy(synth.CHAINED_TEXT_MAP)
+    prev = _lib.lib().blt_debug_set_pin_ring(1)
+    try:
+        with shared_contexts():
+            got, lens = s.process_chunks(data, cs, n_gpus=n_gpus, return_chunk_lens=True)
+            got_g = g.process_chunks(data[: 40 << 20], cs, n_gpus=n_gpus)
+    finally:
+        _lib.lib().blt_debug_set_pin_ring(prev)
+    assert np.array_equal(got, O.COracle(m).run(data, cs, threads=8))
+    assert int(lens.sum()) == got.size and lens.size == (n + cs - 1) // cs
+    assert np.array_equal(got_g, O.COracle(synth.CHAINED_TEXT_MAP).run(data[: 40 << 20], cs, threads=8))
+
+
 @pytest.mark.parametrize("n_gpus", [2, 3])
 def test_multi_context_general_map(n_gpus):
     """A general map (byte pass + u16 passes, chained on each context's device) over n_gpus

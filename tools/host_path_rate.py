@@ -4,7 +4,8 @@
 
 1. cfg3 through the host-buffer entry point blt_bpe_process_chunks (pageable host input ->
    device -> host output, chunk lengths) at each --gpus n_gpus (device contexts; on a one-GPU box
-   they share the device): the PCIe-inclusive rate.  Never the bench value.
+   they share the device), with and without the pinned staging ring (--pin): the PCIe-inclusive
+   rate.  Never the bench value.
 2. cfg2 (256 merges, 100 MiB text, 16 MiB chunks) on device-resident buffers: kernel rate and
    output tokens per input byte.
 Both outputs are checked bit-exactly against the C oracle.
@@ -50,6 +51,7 @@ def main():
     ap.add_argument("--gpus", default="1,8", help="n_gpus values for blt_bpe_process_chunks (contexts; on a one-GPU "
                                                    "box they share the device)")
     ap.add_argument("--no-cfg2", action="store_true")
+    ap.add_argument("--pin", default="0,1", help="pinned staging ring off/on (blt_debug_set_pin_ring)")
     a = ap.parse_args()
     import blt_amd
     from blt_amd import synth
@@ -68,8 +70,10 @@ def main():
     olen = ctypes.c_size_t(0)
     runs = [(int(x), False) for x in a.gpus.split(",")]
     runs += [(g, True) for g, _ in runs if g > 1]   # n_gpus contexts sharing the one device
-    for g, shared in runs:
+    runs = [(g, shared, int(p)) for g, shared in runs for p in a.pin.split(",")]
+    for g, shared, pin in runs:
         L.blt_debug_set_shared_contexts(1 if shared else 0)
+        L.blt_debug_set_pin_ring(pin)
 
         def call():
             _lib.check(L.blt_bpe_process_chunks(s3.handle, text.ctypes.data, n, CHUNK, g, out.ctypes.data, out.size,
@@ -82,8 +86,10 @@ def main():
             ts.append(time.perf_counter() - t0)
         dt = min(ts)
         L.blt_debug_set_shared_contexts(0)
-        res[f"cfg3_host_path_n_gpus{g}" + ("_shared_contexts" if shared else "")] = {
+        L.blt_debug_set_pin_ring(0)
+        res[f"cfg3_host_path_n_gpus{g}" + ("_shared_contexts" if shared else "") + ("_pinned_ring" if pin else "")] = {
                                             "bytes": n, "n_gpus": g, "contexts": g if shared else 1,
+                                            "pinned_ring": bool(pin),
                                             "seconds": round(dt, 4),
                                             "seconds_all": [round(t, 4) for t in ts],
                                             "GBps": round(n / dt / 1e9, 3),
