@@ -512,21 +512,27 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
     // Upload on a private stream and wait for it: the kernels run on non-blocking streams,
     // which do not order behind null-stream copies.
     std::call_once(t.once, [&]() {
+        // one allocation and one copy (separate ones cost the CLI's start-up: profiles/r05_cli_phases.json)
+        auto up256 = [](size_t x) { return (x + 255) & ~size_t(255); };
+        const size_t b_dense = 65536 * sizeof(uint16_t), b_self = blt::kSelfEntries * sizeof(uint16_t);
+        const size_t b_hash = h->hwords.size() * sizeof(uint32_t);
+        const size_t o_ne = up256(b_dense), o_be = o_ne + up256(b_self), o_hash = o_be + up256(b_self);
+        const size_t total = o_hash + up256(b_hash);
+        std::vector<uint8_t> blob(total, 0);
+        memcpy(blob.data(), h->dense.data(), b_dense);
+        memcpy(blob.data() + o_ne, h->self_ne.data(), b_self);
+        memcpy(blob.data() + o_be, h->self_be.data(), b_self);
+        if (b_hash) memcpy(blob.data() + o_hash, h->hwords.data(), b_hash);
         hipStream_t us = nullptr;
+        uint8_t* base = nullptr;
         bool ok = hipStreamCreateWithFlags(&us, hipStreamNonBlocking) == hipSuccess &&
-                  hipMalloc(&t.dense, 65536 * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.dense, h->dense.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice, us) ==
-                      hipSuccess &&
-                  hipMalloc(&t.self_ne, blt::kSelfEntries * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.self_ne, h->self_ne.data(), blt::kSelfEntries * sizeof(uint16_t), hipMemcpyHostToDevice,
-                                 us) == hipSuccess &&
-                  hipMalloc(&t.self_be, blt::kSelfEntries * sizeof(uint16_t)) == hipSuccess &&
-                  hipMemcpyAsync(t.self_be, h->self_be.data(), blt::kSelfEntries * sizeof(uint16_t), hipMemcpyHostToDevice,
-                                 us) == hipSuccess;
-        if (ok && !h->hwords.empty()) {
-            const size_t bytes = h->hwords.size() * sizeof(uint32_t);
-            ok = hipMalloc(&t.hbuckets, bytes) == hipSuccess &&
-                 hipMemcpyAsync(t.hbuckets, h->hwords.data(), bytes, hipMemcpyHostToDevice, us) == hipSuccess;
+                  hipMalloc(&base, total) == hipSuccess &&
+                  hipMemcpyAsync(base, blob.data(), total, hipMemcpyHostToDevice, us) == hipSuccess;
+        if (base) {   // (blt_bpe_destroy frees `dense`, the allocation's start)
+            t.dense = reinterpret_cast<uint16_t*>(base);
+            t.self_ne = reinterpret_cast<uint16_t*>(base + o_ne);
+            t.self_be = reinterpret_cast<uint16_t*>(base + o_be);
+            if (b_hash) t.hbuckets = reinterpret_cast<uint2*>(base + o_hash);
         }
         ok = ok && hipStreamSynchronize(us) == hipSuccess;
         if (us) (void)hipStreamDestroy(us);
@@ -584,7 +590,8 @@ struct WsLayout {
     uint64_t ctl, status, total, off_a, off_b, cmap, gstat, bytes, zero_bytes;
     // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
     // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
-    uint64_t sp_holes, sp_bits0, sp_bits1, sp_bits2, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles;
+    uint64_t sp_holes, sp_bits0, sp_bits1, sp_bits2, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles,
+        sp_slices;
     uint32_t sp_cap;
 };
 // Longest chain enqueued without reading the pass count (deeper chains run in host-checked batches).
@@ -636,7 +643,9 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
         L.sp_tileo = L.sp_merges + up16(12 * cap);
         L.sp_status = L.sp_tileo + up16(4 * ((sptiles + 15) & ~15ull) + 16);
         L.sp_ctr = L.sp_status + up16(8 * sptiles);
-        L.bytes = L.sp_ctr + up16(4ull * kSparseCtrWords) + 4ull * blt::kSparseSampleBlocks;   // + the gate's sample
+        // + the gate's sample, then the list slices' counts: seeds (two, alternating by pass), merges
+        L.sp_slices = L.sp_ctr + up16(4ull * kSparseCtrWords) + 4ull * blt::kSparseSampleBlocks;
+        L.bytes = L.sp_slices + 3ull * 4ull * blt::kSparseSlices;
     }
     return L;
 }
@@ -918,7 +927,19 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     uint32_t* bits[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_bits1), reinterpret_cast<uint32_t*>(ws + L.sp_bits2)};
     // pass p reads list p & 1 (pass 0's from sparse_list_kernel); its seed bitmap is detect's bits0
     // for pass 0, then bits[(p - 1) & 1], which pass p - 1 wrote (and pass p's apply kernel clears)
+    // list slices: one per wave of the region kernel, at least 256 entries each (small inputs run
+    // fewer waves)
+    {
+        uint32_t nsl = std::min<uint32_t>(blt::kSparseSlices, (q.cap / 256u) & ~3u);
+        if (nsl < 4) nsl = 4;
+        q.nslices = nsl;
+        q.slice = q.cap / nsl;
+    }
+    uint32_t* cnts = reinterpret_cast<uint32_t*>(ws + L.sp_slices);
+    q.cnt_merges = cnts + 2 * blt::kSparseSlices;
     auto at_pass = [&](uint32_t pp) {   // pass pp's lists and counters
+        q.cnt_in = pp ? cnts + ((pp - 1) & 1) * blt::kSparseSlices : nullptr;
+        q.cnt_seeds = cnts + (pp & 1) * blt::kSparseSlices;
         q.seeds_in = seeds[pp & 1];
         q.bits_in = pp ? bits[(pp - 1) & 1] : bits0;
         q.nseeds_in = ctr + 2 + pp;
@@ -1387,18 +1408,21 @@ int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs, bo
     if (!P.stream) HIP_TRY(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
     if (!P.counted) HIP_TRY(hipEventCreateWithFlags(&P.counted, hipEventDisableTiming));
     if (P.win < win || P.ws_bytes < L.bytes || P.nch < nch) {
-        if (P.d_in) (void)hipFree(P.d_in);
-        if (P.d_out) (void)hipFree(P.d_out);
-        if (P.d_ws) (void)hipFree(P.d_ws);
-        if (P.d_off) (void)hipFree(P.d_off);
+        if (P.d_in) (void)hipFree(P.d_in);   // (one allocation: d_out, d_ws, d_off are carved from it)
         if (P.h_rec) (void)hipHostFree(P.h_rec);
         P.d_in = P.d_out = P.d_ws = nullptr;
         P.d_off = P.h_rec = nullptr;
         P.win = P.ws_bytes = P.nch = 0;
-        HIP_TRY(hipMalloc(&P.d_in, up16(win)));
-        HIP_TRY(hipMalloc(&P.d_out, up16(2 * win)));
-        HIP_TRY(hipMalloc(&P.d_ws, L.bytes));
-        HIP_TRY(hipMalloc(&P.d_off, 8 * (nch + 1)));
+        // one device allocation per slot (four separate hipMallocs cost the CLI's start-up ~30 ms
+        // over four slots: profiles/r05_cli_phases.json), 256-byte aligned parts
+        auto up256 = [](uint64_t x) { return (x + 255) & ~255ull; };
+        const uint64_t o_out = up256(win), o_ws = o_out + up256(2 * win), o_off = o_ws + up256(L.bytes);
+        uint8_t* base = nullptr;
+        HIP_TRY(hipMalloc(&base, o_off + up256(8 * (nch + 1))));
+        P.d_in = base;
+        P.d_out = base + o_out;
+        P.d_ws = base + o_ws;
+        P.d_off = reinterpret_cast<uint64_t*>(base + o_off);
         HIP_TRY(hipHostMalloc(&P.h_rec, 8 * (9 + nch + 1), hipHostMallocDefault));
         P.win = win;
         P.ws_bytes = L.bytes;
@@ -1819,10 +1843,7 @@ int blt_bpe_create_from_file(const char* path, blt_bpe** out) {
 void blt_bpe_destroy(blt_bpe* h) {
     if (!h) return;
     for (int d = 0; d < kMaxDevices; ++d) {
-        if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);
-        if (h->dev[d].self_ne) (void)hipFree(h->dev[d].self_ne);
-        if (h->dev[d].self_be) (void)hipFree(h->dev[d].self_be);
-        if (h->dev[d].hbuckets) (void)hipFree(h->dev[d].hbuckets);
+        if (h->dev[d].dense) (void)hipFree(h->dev[d].dense);   // (the tables' one allocation)
     }
     if (uint32_t* w = h->sticky.load(std::memory_order_acquire)) (void)hipHostFree(w);
     for (void* p : h->sp_free) (void)hipHostFree(p);

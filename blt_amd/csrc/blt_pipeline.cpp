@@ -453,12 +453,12 @@ void map_output(int fd, size_t total, size_t est, OutMap* om) {
         om->registered = hipHostRegister(om->m, total, hipHostRegisterDefault) == hipSuccess;
 }
 
-// The output's first `est` bytes mapped writable (MADV_POPULATE_WRITE) by `nt` threads in 2 MiB
-// pieces from the start, once the HIP runtime is up and while the tokeniser runs: the device-to-host
-// copies then mostly land in pages that are already mapped, and where they catch up they fault
-// their own.  Done at start-up (map_output, mode 1), the same page-fault storm held the process's
-// mmap lock against the runtime's own start-up (0.11-0.13 -> 0.23 s); behind it, nothing else
-// maps memory.  Best effort: a piece that fails stops that thread.
+// (experiment, off by default) The output's first `est` bytes mapped writable
+// (MADV_POPULATE_WRITE) by `nt` threads in 2 MiB pieces from the start, once the HIP runtime is up
+// and while the tokeniser runs, so that the device-to-host copies would land in pages already
+// mapped.  Done at start-up (map_output, mode 1), the same page-fault storm held the process's mmap
+// lock against the runtime's own start-up (0.11-0.13 -> 0.23 s); behind it, it contends with the
+// copies themselves (run()).  Best effort: a piece that fails stops that thread.
 void populate_behind(const OutMap& om, size_t est, std::vector<std::thread>& th) {
     const char* tv = getenv("BLT_OUT_THREADS");
     const size_t nt = std::max<size_t>(1, std::min<size_t>(16, (tv && *tv) ? (size_t)atoi(tv) : 4));
@@ -646,6 +646,7 @@ int run(const blt_run_config* c) {
     clock_gettime(CLOCK_MONOTONIC, &ts0);
     const uint8_t* map = nullptr;
     size_t n = 0;
+    int in_populate = 1;
     if (c->input_path) {
         const int fd = ::open(c->input_path, O_RDONLY | O_CLOEXEC);
         if (fd < 0) return os_error(errno);
@@ -676,8 +677,13 @@ int run(const blt_run_config* c) {
             });
         }
         if (n) {
-            // MAP_POPULATE: fault the file in bulk up front, not page by page under the GPU copies
-            void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+            // MAP_POPULATE: fault the file in bulk up front, not page by page under the GPU copies.
+            // (env: A/B runs) BLT_IN_POPULATE=0 maps without it, 2 populates behind the runtime's
+            // start-up instead (as the output: the bulk fault holds the mmap lock the runtime's own
+            // start-up needs)
+            const char* ipv = getenv("BLT_IN_POPULATE");
+            in_populate = (ipv && *ipv) ? atoi(ipv) : 1;
+            void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | (in_populate == 1 ? MAP_POPULATE : 0), fd, 0);
             if (m == MAP_FAILED) {
                 const int e = errno;
                 ::close(fd);
@@ -778,9 +784,22 @@ int run(const blt_run_config* c) {
         ~JoinAll() { for (auto& t : v) if (t.joinable()) t.join(); }
     } join_behind{behind};
     if (direct) {
-        // (env: A/B runs) BLT_OUT_BEHIND=0 leaves every page to the copies' own faults
+        // (env experiment, off: BLT_OUT_BEHIND=1) the output's pages mapped behind the start-up.
+        // Measured (profiles/r05_cli_phases.json): device ready -> chunks written 0.29-0.35 s with
+        // it, 0.24-0.28 s without: the populating threads and the runtime's copies into the same
+        // mapping contend, so the copies fault their own pages.
         const char* pv = getenv("BLT_OUT_POPULATE");
-        if (om.m && !(pv && *pv && atoi(pv) != 0) && env_on("BLT_OUT_BEHIND", true))
+        if (map && in_populate == 2) {   // (env experiment) the input's pages, behind the start-up
+            uint8_t* im = const_cast<uint8_t*>(map);
+            constexpr size_t kPiece = size_t(2) << 20;
+            const size_t pieces = (n + kPiece - 1) / kPiece;
+            for (size_t t = 0; t < 4; ++t)
+                behind.emplace_back([=] {
+                    for (size_t i = t; i < pieces; i += 4)
+                        if (madvise(im + i * kPiece, std::min(kPiece, n - i * kPiece), MADV_POPULATE_READ) != 0) return;
+                });
+        }
+        if (om.m && !(pv && *pv && atoi(pv) != 0) && env_on("BLT_OUT_BEHIND", false))
             populate_behind(om, head + (st.kind == Strategy::kBasic ? 2 * n : n), behind);
         drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om, behind, span_pipe);
     }

@@ -120,9 +120,10 @@ struct SparseParams {
     const uint64_t* gate;       // nonzero: the chain is done or must fall back; every kernel returns
     const uint32_t* cond;       // compaction kernels: run only when *cond == 0 (null: always)
     uint32_t* holes;            // bit p: position p was consumed by a merge (n bits)
-    uint32_t* seeds_in;         // this pass's seeds (positions), count *nseeds_in, bitmap bits_in
-                                // (null: the first pass, seeds = the bitmap bits_in)
+    uint32_t* seeds_in;         // this pass's seeds (positions), bitmap bits_in: the first pass's a
+                                // flat list of *nseeds_in, later passes' per-wave slices (cnt_in)
     uint32_t* nseeds_in;
+    const uint32_t* cnt_in;     // per slice: seeds in it (null: the flat list)
     uint32_t* bits_in;
     uint32_t* seeds_out;        // the next pass's seeds: live tokens this pass made
     uint32_t* nseeds_out;
@@ -130,7 +131,11 @@ struct SparseParams {
     uint32_t* bits_alt;         // the later passes' other seed bitmap (the detect kernel zeroes it)
     uint32_t first_pass;        // 1: the first pass (an overflow leaves everything untouched)
     uint32_t* merges;           // (position, consumed position, value) per merge of this pass
-    uint32_t* nmerges;
+    uint32_t* nmerges;          // totals of the pass (the apply kernel; cap + 1: a slice overflowed)
+    uint32_t* cnt_seeds;        // per slice: next seeds this pass made (the region kernel)
+    uint32_t* cnt_merges;       // per slice: merges this pass made
+    uint32_t slice;             // entries per slice: the region kernel's wave w appends to entries
+    uint32_t nslices;           // [w slice, (w + 1) slice) of seeds_out and merges, no atomics
     uint32_t* flags;            // [0]: a list overflowed (this pass is not applied)
     uint32_t cap;               // entries of each list
     const uint2* hbuckets;      // the map's bucket table (as PassParams)
@@ -153,6 +158,8 @@ struct SparseParams {
     uint32_t zero16;            // sample kernel (16-byte units), ahead of every other sparse kernel
 };
 constexpr uint64_t kSparseTile = 8192;    // positions per compaction tile
+// Region / apply kernels: 256-thread workgroups, one list slice per wave (at most kSparseSlices)
+constexpr uint32_t kSparseSlices = 4096;
 // Positions the detect gate samples: kSparseSampleBlocks evenly spaced runs of 8192 positions.
 constexpr uint32_t kSparseSampleBlocks = 64;
 constexpr uint32_t kSparseSample = kSparseSampleBlocks * 8192u;

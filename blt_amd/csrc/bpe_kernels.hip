@@ -3196,7 +3196,7 @@ __global__ __launch_bounds__(1024) void sparse_sample_kernel(SparseParams q) {
 }
 
 // Bitmap words per workgroup of sparse_list_kernel (whole rounds of 4096, at most kListBlocks
-// workgroups); the detect kernel counts each one's seeds.
+// workgroups).
 constexpr uint32_t kListWords = 16 * 256, kListBlocks = 2048;
 __host__ __device__ __forceinline__ uint64_t sp_list_words(uint64_t nwords) {   // bitmap words per workgroup
     const uint64_t r = (nwords + (uint64_t)kListBlocks * kListWords - 1) / ((uint64_t)kListBlocks * kListWords);
@@ -3206,7 +3206,6 @@ __host__ __device__ __forceinline__ uint64_t sp_list_words(uint64_t nwords) {   
 template <bool kLds>
 __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    __shared__ uint32_t s_cnt[4];
     if (sp_gated(qa)) return;
     SparseParams q = qa;
     q.n = *qa.n_dev;
@@ -3239,110 +3238,89 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
         }
         return v;
     };
-    // 256 words per workgroup and round (block-uniform: one count per round); the round's words
-    // lie in one list workgroup's range (sparse_list_kernel), whose seed count it adds to
-    const uint64_t nwords = (q.n + 31) / 32, lw = sp_list_words(nwords);
+    const uint64_t nwords = (q.n + 31) / 32;
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    for (uint64_t b0 = (uint64_t)blockIdx.x * 256u; b0 < nwords; b0 += stride) {
-        uint32_t nseed = 0;   // this lane's seeds
-        const uint64_t base = b0 + (uint64_t)(threadIdx.x & ~63u);
-        if (base < nwords) {   // (wave-uniform)
-            const uint64_t wd = base + (uint64_t)lane;   // lanes past the end add nothing
-            const uint64_t i0 = wd * 32;
-            uint32_t w[16];
-            if (i0 + 32 <= q.n) {
-                const uint4* src = reinterpret_cast<const uint4*>(q.tok + i0);
+    for (uint64_t base = (uint64_t)blockIdx.x * 256u + (uint64_t)(threadIdx.x & ~63u); base < nwords; base += stride) {
+        const uint64_t wd = base + (uint64_t)lane;   // the loop is wave-uniform; lanes past the end add nothing
+        const uint64_t i0 = wd * 32;
+        uint32_t w[16];
+        if (i0 + 32 <= q.n) {
+            const uint4* src = reinterpret_cast<const uint4*>(q.tok + i0);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint4 v = src[k];
-                    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-                }
-            } else {
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = src[k];
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
+        } else {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t lo = i0 + 2u * k < q.n ? q.tok[i0 + 2u * k] : 0u;
-                    const uint32_t hi = i0 + 2u * k + 1u < q.n ? q.tok[i0 + 2u * k + 1u] : 0u;
-                    w[k] = lo | (hi << 16);
-                }
-            }
-            // the chunk starts in the wave's 2048 positions and the one after (wave-uniform: a binary
-            // search over the sorted chunk starts, then the few in range): this lane's chunk-start
-            // bits, and whether position i0 + 32 starts a chunk
-            const uint64_t W0 = base * 32;
-            uint64_t lo = 0, hi = q.nchunks;
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (q.coff_in[mid] < W0) lo = mid + 1;
-                else hi = mid;
-            }
-            uint32_t csw = 0, nc = 0;
-            for (uint64_t c = lo; c < q.nchunks; ++c) {
-                const uint64_t p = q.coff_in[c];
-                if (p > W0 + 2048) break;
-                if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
-                nc |= p == i0 + 32 ? 1u : 0u;
-            }
-            // lane + 1's first token (wave_shl:1); lane 63 reads it
-            uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
-            if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
-            if (wd < nwords) {
-                uint32_t mask = 0;
-                const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
-#pragma unroll
-                for (int k = 0; k < 32; ++k) {
-                    const uint32_t a = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                    const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
-                    if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
-                }
-                q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
-                q.bits_out[wd] = 0u;
-                q.bits_alt[wd] = 0u;
-                q.holes[wd] = 0u;
-                nseed = (uint32_t)__popc(mask);
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t lo = i0 + 2u * k < q.n ? q.tok[i0 + 2u * k] : 0u;
+                const uint32_t hi = i0 + 2u * k + 1u < q.n ? q.tok[i0 + 2u * k + 1u] : 0u;
+                w[k] = lo | (hi << 16);
             }
         }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) nseed += (uint32_t)__shfl_xor((int)nseed, d, 64);
-        if (lane == 0) s_cnt[threadIdx.x >> 6] = nseed;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t c = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-            if (c) atomicAdd(reinterpret_cast<unsigned long long*>(q.status + b0 / lw), (unsigned long long)c);
+        // the chunk starts in the wave's 2048 positions and the one after (wave-uniform: a binary
+        // search over the sorted chunk starts, then the few in range): this lane's chunk-start
+        // bits, and whether position i0 + 32 starts a chunk
+        const uint64_t W0 = base * 32;
+        uint64_t lo = 0, hi = q.nchunks;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (q.coff_in[mid] < W0) lo = mid + 1;
+            else hi = mid;
         }
-        __syncthreads();   // (s_cnt read)
+        uint32_t csw = 0, nc = 0;
+        for (uint64_t c = lo; c < q.nchunks; ++c) {
+            const uint64_t p = q.coff_in[c];
+            if (p > W0 + 2048) break;
+            if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
+            nc |= p == i0 + 32 ? 1u : 0u;
+        }
+        // lane + 1's first token (wave_shl:1); lane 63 reads it
+        uint32_t nt = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(w[0] & 0xFFFFu), 0x130, 0xF, 0xF, false);
+        if (lane == 63) nt = i0 + 32 < q.n ? q.tok[i0 + 32] : 0u;
+        if (wd < nwords) {
+            uint32_t mask = 0;
+            const uint32_t cut = (csw >> 1) | (nc << 31);   // bit k: position k + 1 starts a chunk
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                const uint32_t a = (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t b = k < 31 ? (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu : nt;
+                if (i0 + k + 1 < q.n && ((cut >> k) & 1u) == 0u && (lookup(a | (b << 16)) >> 31)) mask |= 1u << k;
+            }
+            q.bits_in[wd] = mask;   // the bitmaps of these positions, written whole (no memsets)
+            q.bits_out[wd] = 0u;
+            q.bits_alt[wd] = 0u;
+            q.holes[wd] = 0u;
+        }
     }
 }
 
 // The first pass's seed list from the detect kernel's bitmap.  A workgroup per kListBlocks-th of
 // the bitmap (whole rounds of 4096 words; 16 consecutive words per thread and round, four 16-byte
-// loads); the detect kernel added each round's seeds to the count of the list workgroup whose
-// words they are (one atomic per 256 words), so a workgroup's place in the list is the sum of the
-// counts before it, read at once (at most kListBlocks words), and its seeds go out in position
-// order with one workgroup scan per round.  (A first pass that reads its bitmap directly, a lane per
-// word, measured 549 us on selfval against 20 us from this list: a lane walks its word's seeds one
-// after another, and a long run's seeds sit in few words.  Lists with one atomic per workgroup on
-// the list's counter: 31-45 us, the atomics serialised (~11 ns each on one word:
-// tools/atomic_probe.hip); with a look-back over the workgroups, all resident at once: 18.5 us; counts added by detect's
-// waves, one atomic each: list 11 us, detect +20 us.)
-// The counts are the compaction's status words (zeroed with the run's counters), which the move
-// kernel later marks with another bit.
+// loads): it counts its seeds, publishes the count in its status word, and sums the published
+// counts of the workgroups before it (at most kListBlocks - 1 words, read at once by its threads):
+// its place in the list.  Its seeds then go out in position order, one workgroup scan per round.
+// Workgroups run in blockIdx order on every XCD, so every count waited for is published by a
+// running or finished workgroup.  (A first pass that reads its bitmap directly, a lane per word,
+// measured 549 us on selfval against 20 us from this list: a lane walks its word's seeds one after
+// another, and a long run's seeds sit in few words.  On selfval: rounds of 256 words and one atomic
+// per workgroup on the list's counter, 45 us; one round, 31 us (the atomics serialise, ~11 ns each
+// on one word: tools/atomic_probe.hip); a look-back over 64 predecessors per round trip, 18.5 us
+// (every workgroup is resident at once, so inclusive prefixes spread slowly); counts added by the
+// detect kernel, 11 us here but +20-24 us there.)  The status words are the compaction's (zeroed
+// with the run's counters); the move kernel later marks them with another bit.
+constexpr uint64_t kListPub = 1ull << 62;   // a list workgroup's count is published
 __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_pre[4];
+    __shared__ uint32_t s_bad;
     if (sp_gated(qa) || (*qa.flags & 2u)) return;   // (the detect gate: not taken)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
     const uint64_t nwords = (*qa.n_dev + 31) / 32, per = sp_list_words(nwords);
     const uint64_t wb0 = (uint64_t)b * per, wb1 = wb0 + per < nwords ? wb0 + per : nwords;
-    if (wb0 >= nwords) return;   // (uniform)
-    uint32_t pre = 0;   // seeds of the workgroups before this one
-    for (uint32_t k = tid; k < b; k += 256) pre += (uint32_t)qa.status[k];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) pre += (uint32_t)__shfl_xor((int)pre, d, 64);
-    if (lane == 0) s_pre[wave] = pre;
-    uint32_t base = 0;   // (set after the first barrier)
-    for (uint64_t r0 = wb0; r0 < wb1; r0 += kListWords) {   // (uniform)
-        const uint64_t w0 = r0 + 16ull * tid;
-        uint32_t m[16];
+    if (wb0 >= nwords) return;   // (uniform; no later workgroup has words either)
+    auto load16 = [&](uint64_t w0, uint32_t (&m)[16]) {
         if (w0 + 16 <= wb1) {   // (the bitmaps are 16-byte aligned)
             const uint4* src = reinterpret_cast<const uint4*>(qa.bits_in + w0);
 #pragma unroll
@@ -3354,13 +3332,61 @@ __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) m[k] = w0 + k < wb1 ? qa.bits_in[w0 + k] : 0u;
         }
+    };
+    auto popc16 = [](const uint32_t (&m)[16]) {
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c += (uint32_t)__popc(m[k]);
+        return c;
+    };
+    // this workgroup's count (the first round stays in registers)
+    uint32_t m[16];
+    load16(wb0 + 16ull * tid, m);
+    const uint32_t c0 = popc16(m);
+    uint32_t call = c0;
+    for (uint64_t r0 = wb0 + kListWords; r0 < wb1; r0 += kListWords) {
+        uint32_t t[16];
+        load16(r0 + 16ull * tid, t);
+        call += popc16(t);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) call += (uint32_t)__shfl_xor((int)call, d, 64);
+    if (lane == 0) s_w[wave] = call;
+    if (tid == 0) s_bad = 0u;
+    __syncthreads();
+    if (tid == 0) st_publish(qa.status + b, kListPub | (uint64_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
+    // the counts before this workgroup
+    uint32_t pre = 0;
+    bool bad = false;
+    for (uint32_t k = tid; k < b; k += 256) {
+        uint64_t v = st_read(qa.status + k);
+        SpinClock clk;
+        while ((v & kListPub) == 0ull) {
+            if (clk.expired()) { bad = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+            v = st_read(qa.status + k);
+        }
+        pre += (uint32_t)v;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) pre += (uint32_t)__shfl_xor((int)pre, d, 64);
+    if (lane == 0) s_pre[wave] = pre;
+    if (bad) s_bad = 1u;
+    __syncthreads();
+    if (s_bad) {   // (never expected) dropped as an overflow: the host's passes take over
+        if (tid == 0) atomicOr(qa.flags, 3u);
+        return;
+    }
+    uint32_t base = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
+    if (wb1 == nwords && tid == 0) *qa.nseeds_out = base + s_w[0] + s_w[1] + s_w[2] + s_w[3];   // the list's length
+    for (uint64_t r0 = wb0; r0 < wb1; r0 += kListWords) {   // (uniform)
+        const uint64_t w0 = r0 + 16ull * tid;
+        if (r0 != wb0) load16(w0, m);
+        const uint32_t c = r0 == wb0 ? c0 : popc16(m);
         const uint32_t incl = wave_incl_scan(c, (int)lane);
+        __syncthreads();   // (s_w of the round before read)
         if (lane == 63) s_w[wave] = incl;
         __syncthreads();
-        if (r0 == wb0) base = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];
         uint32_t o = base + incl - c;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) o += k < wave ? s_w[k] : 0u;
@@ -3373,44 +3399,47 @@ __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
                 }
             }
         }
-        __syncthreads();   // (s_w read)
     }
-    if (wb1 == nwords && tid == 0) *qa.nseeds_out = base;   // the last workgroup: the list's length
 }
 
 // One sparse pass: the runs of the seeds' owners, merges and next seeds into lists.  The first pass
-// takes its seeds from the detect kernel's bitmap (a lane per word: up to 32 seeds each, one after
-// the other), the later ones from the list the pass before made.  A wave takes 64 words or list
-// entries; its lanes walk their runs in step, one merge per lane per step, and each step's merges and
-// new seeds are appended with one atomic per list.  An overflow in the first pass sets flag bit 2:
-// nothing is applied and the compaction does not run (the tokens stay as they were).
+// takes its seeds from the flat list of sparse_list_kernel (a wave per 64 entries, grid-stride), the
+// later ones from the slice the same wave of the pass before filled.  The lanes of a wave walk their
+// runs in step, one merge per lane per step, and append each step's merges and new seeds to the
+// wave's own slice of each list (wave w: entries [w slice, (w + 1) slice)), counted in registers; the
+// wave stores its counts at the end.  (Appending to one list with one atomic per wave step on its
+// counter cost ~11 ns per step, serialised on the word: ~20 us for the first pass on selfval.)  A
+// slice that overflows sets the flags (bit 2 in the first pass: nothing is applied and the compaction
+// does not run, the tokens stay as they were) and the pass's merge total to cap + 1.
 __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
     if (sp_gated(qa) || *qa.flags) return;
     SparseParams q = qa;
     q.n = *qa.n_dev;
-    const bool from_bits = q.seeds_in == nullptr;
-    const uint32_t ns = from_bits ? (uint32_t)((q.n + 31) / 32) : min(*q.nseeds_in, q.cap);
     const uint32_t oflag = q.first_pass ? 3u : 1u;
     const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);   // this wave's slice
     const uint64_t below = (1ull << lane) - 1ull;
-    for (uint32_t base = blockIdx.x * 256u + (threadIdx.x & ~63u); base < ns; base += gridDim.x * 256u) {   // (uniform)
+    uint32_t* const mslice = q.merges + 3ull * w * q.slice;
+    uint32_t* const sslice = q.seeds_out + (uint64_t)w * q.slice;
+    uint32_t nm = 0, nsd = 0;   // merges and next seeds of this wave so far (uniform)
+    const bool flat = q.cnt_in == nullptr;
+    const uint32_t* const src = flat ? q.seeds_in : q.seeds_in + (uint64_t)w * q.slice;
+    const uint32_t ns = flat ? min(*q.nseeds_in, q.cap) : min(q.cnt_in[w], q.slice);
+    const uint32_t b0 = flat ? w * 64u : 0u, bstep = flat ? q.nslices * 64u : 64u;
+    bool over = false;
+    for (uint32_t base = b0; base < ns; base += bstep) {   // (uniform)
         const uint32_t idx = base + (uint32_t)lane;
-        // this lane's pending seeds: a bitmap word's bits (positions 32 idx + bit), or one list entry
+        // this lane's seed (one list entry), if any
         uint32_t pend = 0;
         uint64_t pbase = 0;
         if (idx < ns) {
-            if (from_bits) {
-                pend = q.bits_in[idx];
-                pbase = 32ull * idx;
-            } else {
-                pend = 1u;
-                pbase = q.seeds_in[idx];
-            }
+            pend = 1u;
+            pbase = src[idx];
         }
         bool act = false;
         uint64_t i = 0, c1 = 0;
         while (__ballot(act || pend != 0u) != 0ull) {   // (uniform)
-            if (!act && pend != 0u) {   // the next seed: its run's first position, if this lane owns it
+            if (!act && pend != 0u) {   // the seed: its run's first position, if this lane owns it
                 const uint64_t sd = pbase + (uint64_t)__builtin_ctz(pend);
                 pend &= pend - 1u;
                 if (sd < q.n && !sp_bit(q.holes, sd)) {   // (always: a seed is a token)
@@ -3445,29 +3474,24 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
             }
             const bool mg = act && (v >> 31) != 0u, lv = mg && ((v >> 30) & 1u);
             const uint64_t mm = __ballot(mg), lm = __ballot(lv);
-            uint32_t mb = 0, sb = 0;
-            if (lane == 0) {
-                if (mm) mb = atomicAdd(q.nmerges, (uint32_t)__popcll(mm));
-                if (lm) sb = atomicAdd(q.nseeds_out, (uint32_t)__popcll(lm));
-            }
-            mb = (uint32_t)__shfl((int)mb, 0, 64);
-            sb = (uint32_t)__shfl((int)sb, 0, 64);
             if (mg) {
-                const uint32_t m = mb + (uint32_t)__popcll(mm & below);
-                if (m < q.cap) {
-                    q.merges[3u * m] = (uint32_t)i;
-                    q.merges[3u * m + 1u] = (uint32_t)j;
-                    q.merges[3u * m + 2u] = v & 0xFFFFu;
+                const uint32_t m = nm + (uint32_t)__popcll(mm & below);
+                if (m < q.slice) {
+                    mslice[3u * m] = (uint32_t)i;
+                    mslice[3u * m + 1u] = (uint32_t)j;
+                    mslice[3u * m + 2u] = v & 0xFFFFu;
                 } else {
-                    atomicOr(q.flags, oflag);
+                    over = true;
                 }
             }
             if (lv) {   // a live token: a seed of the next pass
-                const uint32_t so = sb + (uint32_t)__popcll(lm & below);
-                if (so < q.cap) q.seeds_out[so] = (uint32_t)i;
-                else atomicOr(q.flags, oflag);
+                const uint32_t so = nsd + (uint32_t)__popcll(lm & below);
+                if (so < q.slice) sslice[so] = (uint32_t)i;
+                else over = true;
                 atomicOr(&q.bits_out[i >> 5], 1u << (i & 31u));
             }
+            nm += (uint32_t)__popcll(mm);
+            nsd += (uint32_t)__popcll(lm);
             if (act) {
                 act = false;
                 if (mg) {
@@ -3482,26 +3506,63 @@ __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
             }
         }
     }
+    if (lane == 0) {
+        q.cnt_merges[w] = min(nm, q.slice);
+        q.cnt_seeds[w] = min(nsd, q.slice);
+    }
+    if (__ballot(over) != 0ull && lane == 0) {
+        atomicOr(q.flags, oflag);
+        *q.nmerges = q.cap + 1u;   // (the host stops counting applied passes here)
+    }
 }
 
-// The pass's merges applied (unless a list overflowed: then the pass is dropped whole and the host
-// compacts what the earlier passes made), and the pass's seed bits cleared for reuse.
+// The pass's merges applied, a wave per slice (unless a list overflowed: then the pass is dropped
+// whole and the host compacts what the earlier passes made), the pass's seed bits cleared for reuse
+// (later passes: their seed bitmaps alternate), and the pass's totals for the host (workgroup 0).
 __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
+    __shared__ uint32_t s_t[2][4];
     if (sp_gated(q)) return;
-    const uint32_t nm = *q.flags ? 0u : min(*q.nmerges, q.cap);
-    const uint32_t ns = q.seeds_in ? min(*q.nseeds_in, q.cap) : 0u;
-    const uint32_t nmax = nm > ns ? nm : ns;
-    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < nmax; idx += gridDim.x * 256u) {
-        if (idx < nm) {
-            const uint32_t i = q.merges[3u * idx], j = q.merges[3u * idx + 1u];
-            q.tok[i] = (uint16_t)q.merges[3u * idx + 2u];
+    const bool skip = *q.flags != 0u;
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (!skip) {
+        const uint32_t nm = min(q.cnt_merges[w], q.slice);
+        const uint32_t* ms = q.merges + 3ull * w * q.slice;
+        for (uint32_t e = (uint32_t)lane; e < nm; e += 64u) {
+            const uint32_t i = ms[3u * e], j = ms[3u * e + 1u];
+            q.tok[i] = (uint16_t)ms[3u * e + 2u];
             atomicOr(&q.holes[j >> 5], 1u << (j & 31u));
             atomicAdd(&q.tile_cnt[j / kSparseTile], 1u);   // holes per compaction tile
         }
-        if (idx < ns) {   // (the first pass's bitmap is not reused)
-            const uint32_t sd = q.seeds_in[idx];
+    }
+    if (q.cnt_in && !skip) {   // (the first pass's bitmap is not reused; after an overflow the
+                               // counts may be stale, and the next run's detect rewrites the bitmaps)
+        const uint32_t ns = min(q.cnt_in[w], q.slice);
+        const uint32_t* ss = q.seeds_in + (uint64_t)w * q.slice;
+        for (uint32_t e = (uint32_t)lane; e < ns; e += 64u) {
+            const uint32_t sd = ss[e];
             atomicAnd(&q.bits_in[sd >> 5], ~(1u << (sd & 31u)));
         }
+    }
+    if (skip || blockIdx.x != 0) return;
+    uint32_t tm = 0, ts = 0;
+    for (uint32_t k = threadIdx.x; k < q.nslices; k += 256u) {
+        tm += min(q.cnt_merges[k], q.slice);
+        ts += min(q.cnt_seeds[k], q.slice);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        tm += (uint32_t)__shfl_xor((int)tm, d, 64);
+        ts += (uint32_t)__shfl_xor((int)ts, d, 64);
+    }
+    if (lane == 0) {
+        s_t[0][threadIdx.x >> 6] = tm;
+        s_t[1][threadIdx.x >> 6] = ts;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *q.nmerges = s_t[0][0] + s_t[0][1] + s_t[0][2] + s_t[0][3];
+        *q.nseeds_out = s_t[1][0] + s_t[1][1] + s_t[1][2] + s_t[1][3];
     }
 }
 
@@ -3518,15 +3579,13 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
 // selfval against ~10 ns per ticket): every XCD dispatches its workgroups in order, so the lowest
 // unfinished tile is running and waits for nobody, and a wait on a lower tile always ends.
 constexpr int kCpThreads = 256;
-constexpr uint64_t kMvRead = 1ull << 61;   // a tile's input is read (the list kernel's counts stay below it)
+constexpr uint64_t kMvRead = 1ull << 61;   // a tile's input is read (the list kernel's published counts use bit 62)
 static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
 static_assert(kSparseSampleBlocks == 64, "the detect gate sums the sample with one wave");
 
 // The tiles' hole counts turned in place into the holes before each tile, and the total into
-// *super_cnt: one workgroup.  Up to 64 Ki tiles (2^29 positions) in one round: each thread loads
-// its run of up to 64 consecutive counts at once (16-byte loads), one workgroup scan; larger
-// counts in rounds of 64 Ki tiles with the carry between them.  (Rounds of 16 Ki tiles, 16 counts
-// per thread: 8.6 us on selfval's 33 K tiles.)
+// *super_cnt: one workgroup, 16 consecutive counts per thread (four 16-byte loads, lanes on
+// consecutive 64 bytes), rounds of 16384 tiles with the carry between them.
 __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa, const uint32_t* nseeds0) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
@@ -3536,24 +3595,25 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
     const uint64_t nt16 = (ntiles + 15) & ~15ull;   // (the count array is padded: zeroed, 16-byte aligned)
-    constexpr uint32_t kPer = 64, kRound = 1024u * kPer;
     if (tid == 0) s_carry = 0u;
     __syncthreads();
-    for (uint64_t r0 = 0; r0 < nt16; r0 += kRound) {
-        // this round's counts: per thread a run of `per` (a multiple of 4, at most kPer)
-        const uint64_t left = nt16 - r0 < kRound ? nt16 - r0 : kRound;
-        const uint32_t per = (uint32_t)(((left + 1023) / 1024 + 3) & ~3ull);
-        const uint64_t t0 = r0 + (uint64_t)per * tid;
-        uint32_t c[kPer];
+    for (uint64_t r0 = 0; r0 < nt16; r0 += 16 * 1024) {
+        const uint64_t t0 = r0 + 16ull * tid;
+        uint32_t c[16];
+        if (t0 < nt16) {
+            const uint4* src = reinterpret_cast<const uint4*>(q.tile_cnt + t0);
 #pragma unroll
-        for (uint32_t k = 0; k < kPer / 4; ++k) {
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (4 * k < per && t0 + 4 * k < nt16) v = *reinterpret_cast<const uint4*>(q.tile_cnt + t0 + 4 * k);
-            c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = src[k];
+                c[4 * k] = v.x; c[4 * k + 1] = v.y; c[4 * k + 2] = v.z; c[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c[k] = 0u;
         }
         uint32_t h = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) h += c[k];
+        for (int k = 0; k < 16; ++k) h += c[k];
         const uint32_t incl = wave_incl_scan(h, (int)lane);
         if (lane == 63) s_w[wave] = incl;
         __syncthreads();
@@ -3565,16 +3625,16 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
             tot += v;
         }
         before += incl - h;
+        if (t0 < nt16) {
+            uint32_t o[16];
 #pragma unroll
-        for (uint32_t k = 0; k < kPer / 4; ++k) {
-            uint32_t o[4];
-#pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                o[e] = before;
-                before += c[4 * k + e];
+            for (int k = 0; k < 16; ++k) {
+                o[k] = before;
+                before += c[k];
             }
-            if (4 * k < per && t0 + 4 * k < nt16)
-                *reinterpret_cast<uint4*>(q.tile_cnt + t0 + 4 * k) = make_uint4(o[0], o[1], o[2], o[3]);
+            uint4* dst = reinterpret_cast<uint4*>(q.tile_cnt + t0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dst[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
         }
         __syncthreads();   // (s_w and s_carry read)
         if (tid == 0) s_carry += tot;
@@ -3743,17 +3803,12 @@ hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s) {
-    if (!sparse_ok(q)) return hipErrorInvalidValue;
-    // the first pass: a lane per bitmap word (every word at once: the lanes walk dependent loads);
-    // later passes: lists of a pass's live tokens, mostly short
-    uint64_t rb = 1024;
-    if (!q.seeds_in) {
-        rb = ((q.n + 31) / 32 + 255) / 256;
-        if (rb > 65535) rb = 65535;
-        if (rb < 1) rb = 1;
-    }
-    hipLaunchKernelGGL(sparse_region_kernel, dim3((unsigned)rb), dim3(256), 0, s, q);
-    hipLaunchKernelGGL(sparse_apply_kernel, dim3(q.seeds_in ? 256u : 2048u), dim3(256), 0, s, q);
+    if (!sparse_ok(q) || !q.cnt_seeds || !q.cnt_merges || !q.slice || !q.nslices || q.nslices % 4 ||
+        q.nslices > kSparseSlices || (uint64_t)q.slice * q.nslices > q.cap)
+        return hipErrorInvalidValue;
+    // a wave per slice, the same grid for both kernels (and every pass of the run)
+    hipLaunchKernelGGL(sparse_region_kernel, dim3(q.nslices / 4u), dim3(256), 0, s, q);
+    hipLaunchKernelGGL(sparse_apply_kernel, dim3(q.nslices / 4u), dim3(256), 0, s, q);
     return hipGetLastError();
 }
 hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0, hipStream_t s) {
