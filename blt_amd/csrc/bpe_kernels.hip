@@ -3643,7 +3643,11 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
     if (tid == 0) *q.super_cnt = s_carry;
 }
 
-__global__ __launch_bounds__(kCpThreads) __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef BLT_MOVE_TILES
+#define BLT_MOVE_TILES 1
+#endif
+constexpr int kMoveTiles = BLT_MOVE_TILES;   // consecutive tiles per workgroup, all loaded at once
+__global__ __launch_bounds__(kCpThreads) __attribute__((amdgpu_waves_per_eu(kMoveTiles == 1 ? 8 : 6)))
 void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
     // staged tokens, shifted by the output's offset in its 8-token group so that every output group
     // is one aligned 16-byte LDS word
@@ -3651,98 +3655,111 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
     __shared__ uint32_t s_wsum[4][kCpThreads / 64];
     if (sp_compact_skip(qa, nseeds0)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t n = *qa.n_dev, ntiles = (n + kSparseTile - 1) / kSparseTile, T = blockIdx.x;
-    if (T >= ntiles) return;   // (uniform: the grid is sized for the host's count, >= the device's)
-    const uint64_t tile0 = T * kSparseTile;
-    const uint32_t hb = qa.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
-    const uint32_t hnext = T + 1 < ntiles ? qa.tile_cnt[T + 1] : *qa.super_cnt;
-    // level j: 8-token group G = j * kCpThreads + tid
-    uint32_t w[4][4], valid[4];
+    const uint64_t n = *qa.n_dev, ntiles = (n + kSparseTile - 1) / kSparseTile;
+    const uint64_t T0 = (uint64_t)blockIdx.x * kMoveTiles;
+    if (T0 >= ntiles) return;   // (uniform: the grid is sized for the host's count, >= the device's)
+    // level j of tile t: 8-token group G = j * kCpThreads + tid
+    uint32_t w[kMoveTiles][4][4], valid[kMoveTiles][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
-        const uint64_t p = tile0 + 8ull * G;
-        valid[j] = 0u;
-        w[j][0] = w[j][1] = w[j][2] = w[j][3] = 0u;
-        if (p < n) {
-            const uint64_t left = n - p;
-            valid[j] = ~(qa.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
-            if (left >= 8) {
-                const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(qa.tok + p));
-                w[j][0] = v.x; w[j][1] = v.y; w[j][2] = v.z; w[j][3] = v.w;
+    for (int t = 0; t < kMoveTiles; ++t) {
+        const uint64_t tile0 = (T0 + t) * kSparseTile;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t G = (uint32_t)j * kCpThreads + (uint32_t)tid;
+            const uint64_t p = tile0 + 8ull * G;
+            valid[t][j] = 0u;
+            w[t][j][0] = w[t][j][1] = w[t][j][2] = w[t][j][3] = 0u;
+            if (p < n) {
+                const uint64_t left = n - p;
+                valid[t][j] = ~(qa.holes[p >> 5] >> (8u * (G & 3u))) & (left >= 8 ? 0xFFu : ((1u << left) - 1u));
+                if (left >= 8) {
+                    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(qa.tok + p));
+                    w[t][j][0] = v.x; w[t][j][1] = v.y; w[t][j][2] = v.z; w[t][j][3] = v.w;
+                } else {   // (unrolled: a dynamic index would put w in scratch memory)
+#pragma unroll
+                    for (uint32_t k = 0; k < 7; ++k)
+                        if (k < left) w[t][j][k >> 1] |= (uint32_t)qa.tok[p + k] << (16u * (k & 1u));
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kMoveTiles; ++t) {
+        const uint64_t T = T0 + t;
+        if (T >= ntiles) break;   // (uniform)
+        const uint64_t tile0 = T * kSparseTile;
+        const uint32_t hb = qa.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
+        const uint32_t hnext = T + 1 < ntiles ? qa.tile_cnt[T + 1] : *qa.super_cnt;
+        const uint64_t O = tile0 - hb;
+        const uint32_t e = (uint32_t)(O & 7u);
+        uint32_t cnt[4], incl[4];
+        if (t) __syncthreads();   // (the previous tile's s_out and s_wsum read)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cnt[j] = __popc(valid[t][j]);
+            incl[j] = wave_incl_scan(cnt[j], lane);
+            if (lane == 63) s_wsum[j][wave] = incl[j];
+        }
+        __syncthreads();
+        uint32_t lbase = e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t wb = 0, lt = 0;
+#pragma unroll
+            for (int k = 0; k < kCpThreads / 64; ++k) {
+                const uint32_t v = s_wsum[j][k];
+                wb += k < wave ? v : 0u;
+                lt += v;
+            }
+            uint32_t o = lbase + wb + incl[j] - cnt[j];
+            if (valid[t][j] == 0xFFu && (o & 1u) == 0u) {
+                uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
+                d[0] = w[t][j][0]; d[1] = w[t][j][1]; d[2] = w[t][j][2]; d[3] = w[t][j][3];
             } else {
-                for (uint32_t k = 0; k < left; ++k) w[j][k >> 1] |= (uint32_t)qa.tok[p + k] << (16u * (k & 1u));
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    if ((valid[t][j] >> k) & 1u) s_out[o++] = (uint16_t)(w[t][j][k >> 1] >> (16u * (k & 1u)));
+                }
             }
+            lbase += lt;
         }
-    }
-    const uint64_t O = tile0 - hb;
-    const uint32_t e = (uint32_t)(O & 7u);
-    uint32_t cnt[4], incl[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        cnt[j] = __popc(valid[j]);
-        incl[j] = wave_incl_scan(cnt[j], lane);
-        if (lane == 63) s_wsum[j][wave] = incl[j];
-    }
-    __syncthreads();
-    uint32_t lbase = e;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t wb = 0, lt = 0;
-#pragma unroll
-        for (int k = 0; k < kCpThreads / 64; ++k) {
-            const uint32_t v = s_wsum[j][k];
-            wb += k < wave ? v : 0u;
-            lt += v;
+        const uint32_t ttot = lbase - e;
+        const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
+        __syncthreads();   // staged: every load of the tile done
+        if (tid == 0) {
+            st_publish(qa.status + T, kMvRead);
+            if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(qa.ctl, qa.sticky, 4u);   // counts vs bitmap
         }
-        uint32_t o = lbase + wb + incl[j] - cnt[j];
-        if (valid[j] == 0xFFu && (o & 1u) == 0u) {
-            uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
-            d[0] = w[j][0]; d[1] = w[j][1]; d[2] = w[j][2]; d[3] = w[j][3];
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                if ((valid[j] >> k) & 1u) s_out[o++] = (uint16_t)(w[j][k >> 1] >> (16u * (k & 1u)));
+        // else in place already; an output range past the tile's input (bad counts) writes nothing
+        const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
+        if (!moves) continue;   // (uniform)
+        if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
+            bool bad = false;
+            const uint64_t ulast = ttot ? (O + ttot - 1) / kSparseTile : 0;
+            const uint64_t uend = ulast + 1 < T ? ulast + 1 : T;
+            for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < uend; u += 64) {
+                SpinClock clk;
+                while ((st_read(qa.status + u) & kMvRead) == 0ull) {
+                    if (clk.expired()) { bad = true; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
             }
+            if (__ballot(bad) != 0ull && lane == 0) flag_error(qa.ctl, qa.sticky, 1u);
         }
-        lbase += lt;
-    }
-    const uint32_t ttot = lbase - e;
-    const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
-    __syncthreads();   // staged: every load of the tile done
-    if (tid == 0) {
-        st_publish(qa.status + T, kMvRead);
-        if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(qa.ctl, qa.sticky, 4u);   // counts vs bitmap
-    }
-    // else in place already; an output range past the tile's input (bad counts) writes nothing
-    const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
-    if (!moves) return;   // (uniform)
-    if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
-        bool bad = false;
-        const uint64_t ulast = ttot ? (O + ttot - 1) / kSparseTile : 0;
-        const uint64_t uend = ulast + 1 < T ? ulast + 1 : T;
-        for (uint64_t u = O / kSparseTile + (uint64_t)lane; u < uend; u += 64) {
-            SpinClock clk;
-            while ((st_read(qa.status + u) & kMvRead) == 0ull) {
-                if (clk.expired()) { bad = true; break; }
-                __builtin_amdgcn_s_sleep(1);
+        __syncthreads();
+        // output groups r = 0 .. nr - 1 (global tokens 8 (O / 8 + r) ..): whole ones with one 16-byte
+        // store, the partial first and last token by token
+        const uint32_t nr = (e + ttot + 7u) / 8u;
+        uint16_t* dst = qa.tok + (O - e);
+        for (uint32_t r = (uint32_t)tid; r < nr; r += kCpThreads) {
+            const uint32_t b = 8u * r;
+            if (b >= e && b + 8u <= e + ttot) {
+                const v4u v = *reinterpret_cast<const v4u*>(s_out + b);
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst + b));
+            } else {
+                for (uint32_t k = b; k < b + 8u; ++k)
+                    if (k >= e && k < e + ttot) dst[k] = s_out[k];
             }
-        }
-        if (__ballot(bad) != 0ull && lane == 0) flag_error(qa.ctl, qa.sticky, 1u);
-    }
-    __syncthreads();
-    // output groups r = 0 .. nr - 1 (global tokens 8 (O / 8 + r) ..): whole ones with one 16-byte
-    // store, the partial first and last token by token
-    const uint32_t nr = (e + ttot + 7u) / 8u;
-    uint16_t* dst = qa.tok + (O - e);
-    for (uint32_t r = (uint32_t)tid; r < nr; r += kCpThreads) {
-        const uint32_t b = 8u * r;
-        if (b >= e && b + 8u <= e + ttot) {
-            const v4u v = *reinterpret_cast<const v4u*>(s_out + b);
-            __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst + b));
-        } else {
-            for (uint32_t k = b; k < b + 8u; ++k)
-                if (k >= e && k < e + ttot) dst[k] = s_out[k];
         }
     }
 }
@@ -3815,7 +3832,8 @@ hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0,
     if (!sparse_ok(q) || !q.total || !nseeds0 || !q.nchunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
     hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(1024), 0, s, q, nseeds0);
-    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)ntiles), dim3(kCpThreads), 0, s, q, nseeds0);
+    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)((ntiles + kMoveTiles - 1) / kMoveTiles)), dim3(kCpThreads), 0, s,
+                       q, nseeds0);
     hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q, nseeds0);
     return hipGetLastError();
 }

@@ -53,12 +53,13 @@ def demangle(name):
 
 
 def table(res):
-    rows = ["%-72s %5s %5s %6s %6s %5s %7s" % ("kernel", "VGPR", "SGPR", "vspill", "sspill", "waves", "LDS")]
+    rows = ["%-72s %5s %5s %6s %6s %7s %5s %7s" % ("kernel", "VGPR", "SGPR", "vspill", "sspill", "scratch", "waves",
+                                                     "LDS")]
     for k in sorted(res, key=demangle):
         r = res[k]
-        rows.append("%-72s %5s %5s %6s %6s %5s %7s" % (demangle(k)[:72], r.get("vgprs"), r.get("sgprs"),
-                                                          r.get("vgpr_spill"), r.get("sgpr_spill"), r.get("waves"),
-                                                          r.get("lds")))
+        rows.append("%-72s %5s %5s %6s %6s %7s %5s %7s" % (demangle(k)[:72], r.get("vgprs"), r.get("sgprs"),
+                                                              r.get("vgpr_spill"), r.get("sgpr_spill"), r.get("scratch"),
+                                                              r.get("waves"), r.get("lds")))
     return "\n".join(rows)
 
 
