@@ -646,7 +646,7 @@ int run(const blt_run_config* c) {
     clock_gettime(CLOCK_MONOTONIC, &ts0);
     const uint8_t* map = nullptr;
     size_t n = 0;
-    int in_populate = 1;
+    int in_populate = 2;
     if (c->input_path) {
         const int fd = ::open(c->input_path, O_RDONLY | O_CLOEXEC);
         if (fd < 0) return os_error(errno);
@@ -677,12 +677,14 @@ int run(const blt_run_config* c) {
             });
         }
         if (n) {
-            // MAP_POPULATE: fault the file in bulk up front, not page by page under the GPU copies.
-            // (env: A/B runs) BLT_IN_POPULATE=0 maps without it, 2 populates behind the runtime's
-            // start-up instead (as the output: the bulk fault holds the mmap lock the runtime's own
-            // start-up needs)
+            // The file's pages are mapped in bulk, not page by page under the GPU copies, but only
+            // once the HIP runtime is up (in_populate 2, the default: MADV_POPULATE_READ on helper
+            // threads beside the tokeniser, run()): MAP_POPULATE here (1) held the process's mmap lock
+            // while the runtime started on the prewarm thread, and the runtime came up at 0.12-0.28 s
+            // instead of 0.06-0.10 s (profiles/r05_cli_phases.json).  (env: A/B runs) BLT_IN_POPULATE
+            // 0 leaves the pages to the copies' own faults.
             const char* ipv = getenv("BLT_IN_POPULATE");
-            in_populate = (ipv && *ipv) ? atoi(ipv) : 1;
+            in_populate = (ipv && *ipv) ? atoi(ipv) : 2;
             void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | (in_populate == 1 ? MAP_POPULATE : 0), fd, 0);
             if (m == MAP_FAILED) {
                 const int e = errno;
@@ -697,7 +699,7 @@ int run(const blt_run_config* c) {
     if (timing) {
         timespec ts1;
         clock_gettime(CLOCK_MONOTONIC, &ts1);
-        fprintf(stderr, "blt timing: input open + mmap (MAP_POPULATE) %.4f s\n",
+        fprintf(stderr, "blt timing: input open + mmap %.4f s\n",
                 (double)(ts1.tv_sec - ts0.tv_sec) + 1e-9 * (double)(ts1.tv_nsec - ts0.tv_nsec));
     }
     struct Unmap {
@@ -783,22 +785,22 @@ int run(const blt_run_config* c) {
         std::vector<std::thread>& v;
         ~JoinAll() { for (auto& t : v) if (t.joinable()) t.join(); }
     } join_behind{behind};
+    if (map && in_populate == 2) {   // the input's pages on 4 threads, behind the runtime's start-up
+        uint8_t* im = const_cast<uint8_t*>(map);
+        constexpr size_t kPiece = size_t(2) << 20;
+        const size_t pieces = (n + kPiece - 1) / kPiece;
+        for (size_t t = 0; t < 4; ++t)
+            behind.emplace_back([=] {
+                for (size_t i = t; i < pieces; i += 4)
+                    if (madvise(im + i * kPiece, std::min(kPiece, n - i * kPiece), MADV_POPULATE_READ) != 0) return;
+            });
+    }
     if (direct) {
         // (env experiment, off: BLT_OUT_BEHIND=1) the output's pages mapped behind the start-up.
         // Measured (profiles/r05_cli_phases.json): device ready -> chunks written 0.29-0.35 s with
         // it, 0.24-0.28 s without: the populating threads and the runtime's copies into the same
         // mapping contend, so the copies fault their own pages.
         const char* pv = getenv("BLT_OUT_POPULATE");
-        if (map && in_populate == 2) {   // (env experiment) the input's pages, behind the start-up
-            uint8_t* im = const_cast<uint8_t*>(map);
-            constexpr size_t kPiece = size_t(2) << 20;
-            const size_t pieces = (n + kPiece - 1) / kPiece;
-            for (size_t t = 0; t < 4; ++t)
-                behind.emplace_back([=] {
-                    for (size_t i = t; i < pieces; i += 4)
-                        if (madvise(im + i * kPiece, std::min(kPiece, n - i * kPiece), MADV_POPULATE_READ) != 0) return;
-                });
-        }
         if (om.m && !(pv && *pv && atoi(pv) != 0) && env_on("BLT_OUT_BEHIND", false))
             populate_behind(om, head + (st.kind == Strategy::kBasic ? 2 * n : n), behind);
         drc = run_mmap_direct(st, map, n, cs, ofd, head, tok, om, behind, span_pipe);
