@@ -3203,6 +3203,7 @@ __host__ __device__ __forceinline__ uint64_t sp_list_words(uint64_t nwords) {   
     return (r ? r : 1ull) * kListWords;
 }
 
+constexpr uint64_t kDetectCsLds = 2048;   // chunk starts the detect kernel stages in LDS (16 KiB)
 template <bool kLds>
 __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
@@ -3221,12 +3222,22 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
     }
     const int lane = threadIdx.x & 63;
     const uint2* tab = q.hbuckets;
-    if constexpr (kLds) {
-        const uint32_t nw = q.hbytes / 4;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(q.hbuckets);
-        for (uint32_t w = threadIdx.x; w < nw; w += 256) s_dyn[w] = src[w];
+    // the chunk starts in LDS after the table (up to kDetectCsLds of them): each wave's binary
+    // search then costs LDS round trips, not global ones (four dependent loads per wave on selfval's
+    // 16 chunks, longer than the wave's own token loads)
+    const bool cs_lds = q.nchunks <= kDetectCsLds;
+    uint64_t* const s_cs = reinterpret_cast<uint64_t*>(s_dyn + (kLds ? ((q.hbytes + 15u) & ~15u) / 4u : 0u));
+    if (kLds || cs_lds) {
+        if (kLds) {
+            const uint32_t nw = q.hbytes / 4;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(q.hbuckets);
+            for (uint32_t w = threadIdx.x; w < nw; w += 256) s_dyn[w] = src[w];
+        }
+        if (cs_lds)
+            for (uint32_t i = threadIdx.x; i < q.nchunks; i += 256) s_cs[i] = q.coff_in[i];
         __syncthreads();
     }
+    const uint64_t* const cs = cs_lds ? s_cs : q.coff_in;
     auto lookup = [&](uint32_t key) -> uint32_t {
         const uint32_t b1 = bucket_hash(key, q.hmul1, q.hshift);
         const uint2 x = kLds ? reinterpret_cast<const uint2*>(s_dyn)[b1] : tab[b1];
@@ -3266,12 +3277,12 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
         uint64_t lo = 0, hi = q.nchunks;
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if (q.coff_in[mid] < W0) lo = mid + 1;
+            if (cs[mid] < W0) lo = mid + 1;
             else hi = mid;
         }
         uint32_t csw = 0, nc = 0;
         for (uint64_t c = lo; c < q.nchunks; ++c) {
-            const uint64_t p = q.coff_in[c];
+            const uint64_t p = cs[c];
             if (p > W0 + 2048) break;
             if (p >= i0 && p < i0 + 32) csw |= 1u << (uint32_t)(p - i0);
             nc |= p == i0 + 32 ? 1u : 0u;
@@ -3315,8 +3326,13 @@ __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_pre[4];
     __shared__ uint32_t s_bad;
-    if (sp_gated(qa) || (*qa.flags & 2u)) return;   // (the detect gate: not taken)
+    if (sp_gated(qa)) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
+    // (the detect gate: not taken) read once for the workgroup: another workgroup of this kernel may
+    // set the flags meanwhile, and every wave must reach the barriers below
+    if (tid == 0) s_bad = *qa.flags & 2u;
+    __syncthreads();
+    if (s_bad) return;
     const uint64_t nwords = (*qa.n_dev + 31) / 32, per = sp_list_words(nwords);
     const uint64_t wb0 = (uint64_t)b * per, wb1 = wb0 + per < nwords ? wb0 + per : nwords;
     if (wb0 >= nwords) return;   // (uniform; no later workgroup has words either)
@@ -3352,8 +3368,7 @@ __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) call += (uint32_t)__shfl_xor((int)call, d, 64);
     if (lane == 0) s_w[wave] = call;
-    if (tid == 0) s_bad = 0u;
-    __syncthreads();
+    __syncthreads();   // (s_bad is 0 here)
     if (tid == 0) st_publish(qa.status + b, kListPub | (uint64_t)(s_w[0] + s_w[1] + s_w[2] + s_w[3]));
     // the counts before this workgroup
     uint32_t pre = 0;
@@ -3412,8 +3427,15 @@ __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
 // slice that overflows sets the flags (bit 2 in the first pass: nothing is applied and the compaction
 // does not run, the tokens stay as they were) and the pass's merge total to cap + 1.
 __global__ __launch_bounds__(256) void sparse_region_kernel(SparseParams qa) {
-    if (sp_gated(qa) || *qa.flags) return;
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_rcs[];   // the chunk starts (kDetectCsLds)
     SparseParams q = qa;
+    if (q.nchunks <= kDetectCsLds) {   // (before the flags test: other workgroups may set the flags
+                                       // meanwhile, and every wave must reach the barrier)
+        for (uint32_t i = threadIdx.x; i < q.nchunks; i += 256) s_rcs[i] = q.coff_in[i];
+        __syncthreads();
+        q.coff_in = s_rcs;   // (a seed's chunk: binary search in LDS)
+    }
+    if (sp_gated(qa) || *qa.flags) return;
     q.n = *qa.n_dev;
     const uint32_t oflag = q.first_pass ? 3u : 1u;
     const int lane = threadIdx.x & 63;
@@ -3804,10 +3826,11 @@ hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
     if (blocks > 2048 && !(lds && q.hbytes <= 4096)) blocks = 2048;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(sparse_sample_kernel, dim3(kSparseSampleBlocks), dim3(1024), 0, s, q);
+    const size_t smem = (lds ? ((q.hbytes + 15u) & ~15u) : 0u) + (q.nchunks <= kDetectCsLds ? 8 * q.nchunks : 0);
     if (lds)
-        hipLaunchKernelGGL(sparse_detect_kernel<true>, dim3((unsigned)blocks), dim3(256), q.hbytes, s, q);
+        hipLaunchKernelGGL(sparse_detect_kernel<true>, dim3((unsigned)blocks), dim3(256), smem, s, q);
     else
-        hipLaunchKernelGGL(sparse_detect_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, q);
+        hipLaunchKernelGGL(sparse_detect_kernel<false>, dim3((unsigned)blocks), dim3(256), smem, s, q);
     return hipGetLastError();
 }
 hipError_t launch_sparse_list(const SparseParams& q, hipStream_t s) {
@@ -3824,7 +3847,8 @@ hipError_t launch_sparse_pass(const SparseParams& q, hipStream_t s) {
         q.nslices > kSparseSlices || (uint64_t)q.slice * q.nslices > q.cap)
         return hipErrorInvalidValue;
     // a wave per slice, the same grid for both kernels (and every pass of the run)
-    hipLaunchKernelGGL(sparse_region_kernel, dim3(q.nslices / 4u), dim3(256), 0, s, q);
+    hipLaunchKernelGGL(sparse_region_kernel, dim3(q.nslices / 4u), dim3(256),
+                       q.nchunks <= kDetectCsLds ? 8 * q.nchunks : 0, s, q);
     hipLaunchKernelGGL(sparse_apply_kernel, dim3(q.nslices / 4u), dim3(256), 0, s, q);
     return hipGetLastError();
 }
