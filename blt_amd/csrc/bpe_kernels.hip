@@ -3590,16 +3590,17 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
 
 // Compaction of the hole layout in place.  The apply kernels counted the holes per tile of 8192
 // positions; one workgroup scans the counts (a tile's output position is its first position less the
-// holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per tile,
-// in blockIdx order (8192 positions: 8-token groups, four per thread, consecutive lanes on
-// consecutive groups), loads its input, stages its tokens in LDS, marks its input read, waits until
-// every earlier tile whose input its output range overlaps has marked its own (the output of tile T
-// lies in [0, end of T's input): the one or two tiles its range falls in), and writes the range with
-// 16-byte stores (2-byte ones at the two partial ends, which the neighbouring tiles share).  Small
-// workgroups, many per CU (eight waves per SIMD): the loads of the tiles in flight hide each other's
-// latency.  Tiles in blockIdx order, not from a ticket (one atomic per tile on one word: 399 us on
-// selfval against ~10 ns per ticket): every XCD dispatches its workgroups in order, so the lowest
-// unfinished tile is running and waits for nobody, and a wait on a lower tile always ends.
+// holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per
+// kMoveTiles consecutive tiles, in blockIdx order (8192 positions a tile: 8-token groups, four per
+// thread, consecutive lanes on consecutive groups), loads their input at once and marks it read, then
+// per tile stages its tokens in LDS, waits until every earlier tile whose input its output range
+// overlaps has marked its own (the output of tile T lies in [0, end of T's input): the one or two
+// tiles its range falls in), and writes the range with 16-byte stores (2-byte ones at the two partial
+// ends, which the neighbouring tiles share).  Small workgroups, many per CU (seven waves per SIMD):
+// the loads of the tiles in flight hide each other's latency.  Tiles in blockIdx order, not from a
+// ticket (one atomic per tile on one word: 399 us on selfval, ~11 ns per ticket): every XCD dispatches
+// its workgroups in order, so the lowest unfinished tile is running and waits for nobody, and a wait
+// on a lower tile always ends.
 constexpr int kCpThreads = 256;
 constexpr uint64_t kMvRead = 1ull << 61;   // a tile's input is read (the list kernel's published counts use bit 62)
 static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
@@ -3665,10 +3666,9 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
     if (tid == 0) *q.super_cnt = s_carry;
 }
 
-#ifndef BLT_MOVE_TILES
-#define BLT_MOVE_TILES 1
-#endif
-constexpr int kMoveTiles = BLT_MOVE_TILES;   // consecutive tiles per workgroup, all loaded at once
+// Two consecutive tiles per workgroup, both loaded at once (twice the loads in flight per
+// workgroup at 7 waves per SIMD: selfval 0.699-0.710 -> 0.694 ms; four tiles spill)
+constexpr int kMoveTiles = 2;
 __global__ __launch_bounds__(kCpThreads) __attribute__((amdgpu_waves_per_eu(kMoveTiles == 1 ? 8 : 6)))
 void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
     // staged tokens, shifted by the output's offset in its 8-token group so that every output group
@@ -3704,6 +3704,14 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
                 }
             }
         }
+    }
+    if (kMoveTiles > 1) {
+        // every tile of the workgroup marked read at once: a mark published only when the tile's
+        // turn comes chains the workgroups (the first tile of workgroup b waits for the last one
+        // of workgroup b - 1, which waits for its first ...: measured 30.8 ms on selfval)
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): every load of the workgroup's tiles
+        __syncthreads();
+        if (tid < kMoveTiles && T0 + tid < ntiles) st_publish(qa.status + T0 + tid, kMvRead);
     }
 #pragma unroll
     for (int t = 0; t < kMoveTiles; ++t) {
@@ -3749,7 +3757,7 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
         const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
         __syncthreads();   // staged: every load of the tile done
         if (tid == 0) {
-            st_publish(qa.status + T, kMvRead);
+            if (kMoveTiles == 1) st_publish(qa.status + T, kMvRead);
             if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(qa.ctl, qa.sticky, 4u);   // counts vs bitmap
         }
         // else in place already; an output range past the tile's input (bad counts) writes nothing
