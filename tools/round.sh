@@ -21,6 +21,7 @@
 #   pmcf2:ROW[:GROUPS] PMC of one f2 row (tools/f2_row.py: every kernel of its calls, traffic per call)
 #   cli[:ENV]          tools/cli_phases.py: the CLI's BLT_CLI_TIMING phases on 1 GiB, the HIP start-up probe
 #   copyprobe          tools/copy_probe.cpp: host<->device copy rates by kind of host memory
+#   rehearse:N         bench.py --gpus N, every rank on device 0 over gloo (multi-rank logic rehearsal)
 #   py:SCRIPT[:ARGS]   a tool script under its own time limit
 #   resources          -Rpass-analysis=kernel-resource-usage of the kernel source (CPU only)
 set -e
@@ -111,6 +112,13 @@ for st in "$@"; do
       [ -x build/copy_probe ] || /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/copy_probe.cpp -o build/copy_probe
       timeout -k 10 120 build/copy_probe > "$O/copy_probe.txt" 2>&1
       cat "$O/copy_probe.txt" ;;
+    rehearse)
+      # rehearse:N  bench.py at --gpus N with every rank on device 0 over gloo (the multi-rank logic on a
+      # one-GPU box; its value is no scaling figure), rehearse_N.json
+      BLT_BENCH_BACKEND=gloo BLT_BENCH_DEVICE=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$a" --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus "$a" --steps 5 --warmup 2 \
+        --no-cpu-baseline --no-extra > "$O/rehearse_$a.json" 2> "$O/rehearse_$a.err"
+      tail -c 600 "$O/rehearse_$a.json" ;;
     py)
       # any tool script: py:tools/x.py[:ARGS] (ARGS + for spaces), output py_<n>.log
       nb=$((nb + 1))
