@@ -1072,6 +1072,40 @@ def _sparse(on):
     return blt_amd._lib.lib().blt_debug_set_sparse(1 if on else 0)
 
 
+def test_sparse_passes_large():
+    """Round 5: the sparse passes past 2^28 tokens: the seed list in two rounds of 4,096 bitmap words
+    per workgroup, the tile-count scan in several rounds, 40 K compaction tiles in blockIdx order two
+    per workgroup, per-wave list slices over the whole grid; self-valued merges on 320 MiB of text in
+    16 MiB chunks, through the device API with chunk offsets, against the oracle."""
+    import torch
+    m, cs = synth.SELF_VALUED_MAP, 16 << 20
+    data = synth.text((320 << 20) + 77, seed=23)
+    exp, elens = O.COracle(m).run(data, cs, threads=16, return_lens=True)
+    s = blt_amd.BpeStrategy(m)
+    n = data.size
+    nch = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+    d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+    wsb = s.workspace_size(n, cs)
+    ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    prev = _sparse(1)
+    try:
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream, d_off.data_ptr(),
+                              sync=True)
+        torch.cuda.synchronize()
+        sp = int(blt_amd._lib.lib().blt_debug_last_sparse())
+    finally:
+        _sparse(prev)
+    assert sp & 0xFFFF and sp & (1 << 16), hex(sp)   # the sparse run was taken and reached the fixpoint
+    assert tok * 2 == exp.size
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    offs = d_off.cpu().numpy()
+    assert np.array_equal(np.diff(offs) * 2, elens)
+    s.check_workspace(ws.data_ptr(), stream)
+
+
 @pytest.mark.parametrize("case", ["selfval_text", "selfval_odd_chunks", "random_cyclic", "random_cyclic_sparse",
                                   "long_tail", "tail_cut_chunks", "tail_nonlive_end", "tiny_cap"])
 def test_sparse_passes(case):
