@@ -506,11 +506,23 @@ int current_device(int* dev) {
     return 0;
 }
 
-int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
+// BLT_CLI_TIMING: a setup step's end (seconds since the first such stamp), on stderr
+void detail_stamp(const char* what) {
+    static const bool on = getenv("BLT_CLI_TIMING") != nullptr;
+    if (!on) return;
+    static timespec t0 = [] { timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t; }();
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "blt timing: detail: %s %.4f s\n", what,
+            (double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec));
+}
+
+int device_tables(const blt_bpe* hc, int dev, DevTables** out, hipStream_t via = nullptr) {
     blt_bpe* h = const_cast<blt_bpe*>(hc);
     DevTables& t = h->dev[dev];
-    // Upload on a private stream and wait for it: the kernels run on non-blocking streams,
-    // which do not order behind null-stream copies.
+    // Upload on a private stream (or the caller's idle stream `via`) and wait for it: the kernels
+    // run on non-blocking streams, which do not order behind null-stream copies.  (Each stream the
+    // process creates costs the CLI's start-up ~10 ms: BLT_CLI_TIMING's detail stamps.)
     std::call_once(t.once, [&]() {
         // one allocation and one copy (separate ones cost the CLI's start-up: profiles/r05_cli_phases.json)
         auto up256 = [](size_t x) { return (x + 255) & ~size_t(255); };
@@ -523,11 +535,15 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
         memcpy(blob.data() + o_ne, h->self_ne.data(), b_self);
         memcpy(blob.data() + o_be, h->self_be.data(), b_self);
         if (b_hash) memcpy(blob.data() + o_hash, h->hwords.data(), b_hash);
-        hipStream_t us = nullptr;
+        hipStream_t us = via;
         uint8_t* base = nullptr;
-        bool ok = hipStreamCreateWithFlags(&us, hipStreamNonBlocking) == hipSuccess &&
-                  hipMalloc(&base, total) == hipSuccess &&
-                  hipMemcpyAsync(base, blob.data(), total, hipMemcpyHostToDevice, us) == hipSuccess;
+        detail_stamp("tables: blob built");
+        bool ok = us || hipStreamCreateWithFlags(&us, hipStreamNonBlocking) == hipSuccess;
+        detail_stamp("tables: stream created");
+        ok = ok && hipMalloc(&base, total) == hipSuccess;
+        detail_stamp("tables: allocated");
+        ok = ok && hipMemcpyAsync(base, blob.data(), total, hipMemcpyHostToDevice, us) == hipSuccess;
+        detail_stamp("tables: copy issued");
         if (base) {   // (blt_bpe_destroy frees `dense`, the allocation's start)
             t.dense = reinterpret_cast<uint16_t*>(base);
             t.self_ne = reinterpret_cast<uint16_t*>(base + o_ne);
@@ -535,7 +551,9 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out) {
             if (b_hash) t.hbuckets = reinterpret_cast<uint2*>(base + o_hash);
         }
         ok = ok && hipStreamSynchronize(us) == hipSuccess;
-        if (us) (void)hipStreamDestroy(us);
+        detail_stamp("tables: copied");
+        if (us && us != via) (void)hipStreamDestroy(us);
+        detail_stamp("tables: stream destroyed");
         if (!ok) t.status = BLT_E_IO;
     });
     if (t.status) return fail(t.status, "uploading merge tables to device %d failed", dev);
@@ -1406,7 +1424,9 @@ int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs, bo
     const uint64_t nch = (win + cs - 1) / cs;
     const WsLayout L = ws_layout(h, win, cs);
     if (!P.stream) HIP_TRY(hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking));
+    detail_stamp("slot: stream");
     if (!P.counted) HIP_TRY(hipEventCreateWithFlags(&P.counted, hipEventDisableTiming));
+    detail_stamp("slot: event");
     if (P.win < win || P.ws_bytes < L.bytes || P.nch < nch) {
         if (P.d_in) (void)hipFree(P.d_in);   // (one allocation: d_out, d_ws, d_off are carved from it)
         if (P.h_rec) (void)hipHostFree(P.h_rec);
@@ -1419,11 +1439,13 @@ int pipe_slot_ready(const blt_bpe* h, PipeSlot& P, uint64_t win, uint64_t cs, bo
         const uint64_t o_out = up256(win), o_ws = o_out + up256(2 * win), o_off = o_ws + up256(L.bytes);
         uint8_t* base = nullptr;
         HIP_TRY(hipMalloc(&base, o_off + up256(8 * (nch + 1))));
+        detail_stamp("slot: device buffer");
         P.d_in = base;
         P.d_out = base + o_out;
         P.d_ws = base + o_ws;
         P.d_off = reinterpret_cast<uint64_t*>(base + o_off);
         HIP_TRY(hipHostMalloc(&P.h_rec, 8 * (9 + nch + 1), hipHostMallocDefault));
+        detail_stamp("slot: pinned record");
         P.win = win;
         P.ws_bytes = L.bytes;
         P.nch = nch;
@@ -2041,16 +2063,17 @@ void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) t
     const uint64_t per_ctx = ((n + win - 1) / win + g - 1) / g;
     const int slots = (int)std::min<uint64_t>(kPipeSlots, per_ctx);
     (void)sticky_word(h);
+    detail_stamp("sticky word");
     for (uint64_t d = 0; d < g; ++d) {
         const int dev = plan.devs[d];
         if (hipSetDevice(dev) != hipSuccess) return;
-        DevTables* t;
-        if (device_tables(h, dev, &t) != 0) return;
-        stamp("device tables");
         DevCtx* c = ctx_acquire(dev);
         if (!c) return;
         CtxGuard guard{c};
         stamp("context (streams)");
+        DevTables* t;
+        if (device_tables(h, dev, &t, c->stream) != 0) return;
+        stamp("device tables");
         if (plan.multi) {
             for (int k = 0; k < slots; ++k)
                 if (pipe_slot_ready(h, c->pipe[k], std::min(win, n), cs) != 0) return;

@@ -354,6 +354,17 @@ struct OutMap {
 // there.  (Page faults under the copies, one per 4 KiB page, were most of the CLI's tokenise phase.)
 void map_output(int fd, size_t total, size_t est, OutMap* om);
 
+// BLT_CLI_TIMING: a step's end, seconds since the first such stamp (stderr)
+void tstamp(const char* what) {
+    static const bool on = getenv("BLT_CLI_TIMING") != nullptr;
+    if (!on) return;
+    static timespec t0 = [] { timespec t; clock_gettime(CLOCK_MONOTONIC, &t); return t; }();
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    fprintf(stderr, "blt timing: step: %s %.4f s\n", what,
+            (double)(t.tv_sec - t0.tv_sec) + 1e-9 * (double)(t.tv_nsec - t0.tv_nsec));
+}
+
 int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, int fd, size_t head,
                     const uint8_t* head_bytes, const OutMap& om, std::vector<std::thread>& behind,
                     const std::string& span) {
@@ -386,13 +397,17 @@ int run_mmap_direct(const Strategy& st, const uint8_t* in, size_t n, size_t cs, 
         }
     }
     if (!rc) log_chunks(span, st.kind == Strategy::kBasic, 0, (n + cs - 1) / cs, n, cs);
+    tstamp("tokens in the output mapping");
     for (auto& t : behind) t.join();   // (populate_behind: done with the mapping too)
     behind.clear();
+    tstamp("helper threads joined");
     if (om.registered) (void)hipHostUnregister(om.m);
     munmap(om.m, total);
+    tstamp("output unmapped");
     const std::string msg = rc ? last_error() : std::string();
     // the bytes produced (an error leaves the content token only, like a run that wrote no chunk)
     if (ftruncate(fd, (off_t)(head + (rc ? 0 : olen))) != 0 && !rc) return os_error(errno);
+    tstamp("output truncated");
     if (rc) return set_error(rc, "%s", msg.c_str());
     return 0;
 }
@@ -705,7 +720,10 @@ int run(const blt_run_config* c) {
     struct Unmap {
         const uint8_t* p;
         size_t n;
-        ~Unmap() { if (p) munmap(const_cast<uint8_t*>(p), n); }
+        ~Unmap() {
+            if (p) munmap(const_cast<uint8_t*>(p), n);
+            tstamp("input unmapped");
+        }
     } unmap{map, n};
 
     // setup_output_writer (io_handler.rs:70-78): File::create truncates; None is stdout.  Created
