@@ -286,6 +286,26 @@ def general_map_rate(blt_amd, synth, O, threads, name="multi", reps=10):
             "bit_exact_vs_oracle": bool(exp.size == got.size and np.array_equal(exp, got))}
 
 
+def cli_phases(stderr, wall):
+    """Seconds of one CLI run's phases from its BLT_CLI_TIMING lines: HIP runtime up, device tables and
+    staging buffers ready, tokens written (from the run's start), and wall - tokens written (the
+    process start before the run, the unmaps and the exit)."""
+    import re
+    st = {}
+    for line in stderr.splitlines():
+        m = re.match(r"blt timing: (.*?) (?:at )?\+?(-?[0-9.]+) s", line)
+        if m:
+            st[m.group(1)] = float(m.group(2))
+    up = st.get("prewarm step: device count (runtime up)")
+    ready = st.get("device ready and output preallocated")
+    done = st.get("chunks written")
+    out = {"runtime_up_s": up, "device_ready_s": ready, "tokens_written_s": done}
+    if ready is not None and done is not None:
+        out["tokenise_s"] = round(done - ready, 4)
+        out["outside_run_s"] = round(wall - done, 4)
+    return out
+
+
 def cli_end_to_end(synth, host, merges, exp):
     """The `blt` binary on cfg3's bytes as a tmpfs file to a tmpfs output (--type text), best of 3
     after one warm run; output bytes checked against the oracle's stream."""
@@ -301,17 +321,20 @@ def cli_end_to_end(synth, host, merges, exp):
         cmd = [os.path.join(ROOT, "blt_amd", "blt"), "-i", fin, "-o", fout, "--merges", fm, "--chunksize", "16MB",
                "--type", "text", "--gpus", "1"]
         subprocess.run(cmd, check=True, timeout=120)
-        ts = []
+        # each timed run also prints its phase stamps (BLT_CLI_TIMING: a few stderr lines)
+        env = dict(os.environ, BLT_CLI_TIMING="1")
+        ts, phases = [], []
         for _ in range(3):
             os.remove(fout)   # a fresh output file: O_TRUNC of the last run's pages is not the tool's cost
             t0 = time.perf_counter()
-            subprocess.run(cmd, check=True, timeout=120)
+            r = subprocess.run(cmd, check=True, timeout=120, env=env, stderr=subprocess.PIPE)
             ts.append(time.perf_counter() - t0)
+            phases.append(cli_phases(r.stderr.decode(errors="replace"), ts[-1]))
         got = np.fromfile(fout, dtype=np.uint8)
         ok = bool(got.size == exp.size + 2 and got[0] == 0xFF and got[1] == 0x01 and np.array_equal(got[2:], exp))
         dt = min(ts)
         return {"value": round(host.size / dt / 1e9, 3), "unit": "GB/s", "seconds": round(dt, 4),
-                "seconds_all": [round(t, 4) for t in ts], "bytes": int(host.size), "tmpfs": base,
+                "seconds_all": [round(t, 4) for t in ts], "phases_all": phases, "bytes": int(host.size), "tmpfs": base,
                 "path": "blt -i IN -o OUT --merges M --chunksize 16MB --type text --gpus 1 (process start to exit: "
                         "merges load, mmap, H2D, kernel, D2H, write)",
                 "bit_exact_vs_oracle": ok}
