@@ -1506,8 +1506,9 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
         HIP_TRY(hipSetDevice(devs[d]));
         ctx[d] = ctx_acquire(devs[d]);
         if (!ctx[d]) return fail(BLT_E_IO, "cannot create a HIP stream on device %d", devs[d]);
-        for (int k = 0; k < slots; ++k)
-            if (int rc = pipe_slot_ready(h, ctx[d]->pipe[k], std::min(win, n), cs, pin)) return rc;
+        // the first slot now, the others by the producer just before their first window: a slot's
+        // stream costs ~8-10 ms to create (a hardware queue), off the first window's path
+        if (int rc = pipe_slot_ready(h, ctx[d]->pipe[0], std::min(win, n), cs, pin)) return rc;
     }
     MultiRun R;
     R.tok.assign(nw, MultiRun::kUnset);
@@ -1526,6 +1527,8 @@ int encode_host_multi(const blt_bpe* h, const std::vector<int>& devs, const uint
                 if (R.rc) return;
             }
             PipeSlot& P = c->pipe[j % slots];
+            if (j > 0 && j < (uint64_t)slots)
+                if (int rc = pipe_slot_ready(h, P, std::min(win, n), cs, pin)) return R.fail_once(rc);
             const uint64_t b0 = w * win, len = std::min(win, n - b0);
             const WsLayout L = ws_layout(h, len, cs);
             int rc = 0;
@@ -2075,8 +2078,8 @@ void blt_prewarm_chunks(const blt_bpe* h, uint64_t n, uint64_t cs, int n_gpus) t
         if (device_tables(h, dev, &t, c->stream) != 0) return;
         stamp("device tables");
         if (plan.multi) {
-            for (int k = 0; k < slots; ++k)
-                if (pipe_slot_ready(h, c->pipe[k], std::min(win, n), cs) != 0) return;
+            // the first slot (blt_bpe_process_chunks readies the others beside its first window)
+            if (slots > 0 && pipe_slot_ready(h, c->pipe[0], std::min(win, n), cs) != 0) return;
             stamp("pipeline slots");
             // the code object's load, off the first window's path
             if (blt::launch_noop(c->pipe[0].stream) == hipSuccess) (void)hipStreamSynchronize(c->pipe[0].stream);
