@@ -806,6 +806,7 @@ constexpr int kS = 2;                                  // sub-tiles per tile
 // cfg5 0.815-0.818 -> 0.804 ms (config_rates, same box); cfg2's 100 MiB, replayed back to back,
 // loses its cache residency (0.0937 -> 0.0955 ms).
 constexpr int kLdPol = 2, kStPol = 2;
+constexpr int kCohPol = 16;   // sc1: a load coherent with other CUs' stores (as an agent-scope atomic load)
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
@@ -1943,17 +1944,44 @@ __device__ __forceinline__ uint64_t cm_word(const uint64_t* cs, uint64_t nc, uin
 constexpr uint32_t kCmLds = 1024;
 __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     __shared__ uint64_t s_cs[kCmLds];
-    const bool done = pass_done(p);      // (both loads in flight together)
-    const uint64_t n = token_count(p);
-    if (done) return;
+    const uint64_t nc = p.nchunks;
+    const bool in_lds = nc <= kCmLds;
+    // the chunk starts are read first, in flight with the pass's two control words below (one
+    // round trip instead of two; a pass that is done reads them for nothing)
+    // the two control words as device-coherent (sc1) buffer loads, without branches around them (an
+    // absent word is a zero-length resource: it reads 0); relaxed atomic loads here each got a
+    // wait of their own
+    // (an offset the compiler cannot see is 0 keeps the words in vector registers: a uniform load
+    // result is moved to a scalar register right after the load, which waits for it there)
+    int z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    const auto nv = __builtin_amdgcn_raw_buffer_load_b64(rsrc_at(p.n_dev, p.n_dev ? 8u : 0u), z, 0, kCohPol);
+    const uint32_t dw = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc_at(p.done, p.done ? 4u : 0u), z, 0, kCohPol);
+    const uint64_t nw = __builtin_bit_cast(uint64_t, nv);
+    constexpr int kPer = (int)(kCmLds / 256u);
+    uint64_t pre[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {   // (cstart holds nc + 1 entries: every index here is valid)
+        const uint64_t i = threadIdx.x + 256u * (uint32_t)q;
+        pre[q] = p.cstart[i < nc ? i : nc];
+    }
+    // every load above issued before the first wait (the scheduler otherwise tests each control word
+    // right after its load)
+    __builtin_amdgcn_sched_barrier(0);
+    const bool done = p.done && dw != 0u;
+    const uint64_t n = p.n_dev ? nw : p.n;
+    // (the exit tests every load, so none is sunk below it: neither n nor a chunk start is ~0)
+    if (done || n == ~0ull || pre[0] == ~0ull) return;
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
     if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
-    const uint64_t nc = p.nchunks;
-    const bool in_lds = nc <= kCmLds;
     if ((uint64_t)blockIdx.x * 256u * kWavePos >= n) return;   // uniform: no range of this block is live
     if (in_lds) {
-        for (uint32_t i = threadIdx.x; i < nc; i += 256u) s_cs[i] = p.cstart[i];
+#pragma unroll
+        for (int q = 0; q < kPer; ++q) {
+            const uint32_t i = threadIdx.x + 256u * (uint32_t)q;
+            if (i < nc) s_cs[i] = pre[q];
+        }
         __syncthreads();
     }
     const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
@@ -2821,8 +2849,11 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         const int32_t rr = (int32_t)n - (int32_t)pos0;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
         uint32_t pairs = (vmask >> 1) | (rr > 16 ? 0x8000u : 0u);
+        // a wave past the group's tokens (uniform: its first position >= n) looks nothing up: the
+        // passes of a chain halve n, so most waves are idle in the later passes
+        const bool wave_on = 1024u * (uint32_t)wave < n;
         uint32_t a_lo = 0;   // first chunk start >= pos0 + 1 (index into s_cpos)
-        if (nc > 1) {
+        if (nc > 1 && wave_on) {
             uint32_t lo = 0, hi = nc;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -2835,16 +2866,18 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
                 pairs &= ~(1u << (b - 1u - pos0));
             }
         }
-        uint32_t v[8], m = 0;
+        uint32_t v[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, m = 0;
+        if (wave_on) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int h = k >> 1;
-            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
-            const uint32_t r = seg::tok_get<kHash>(p, tab, key);
-            const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
-            m |= (uint32_t)hit << k;
-            const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
-            if (k & 1) v[h] |= t << 16; else v[h] = t;
+            for (int k = 0; k < 16; ++k) {
+                const int h = k >> 1;
+                const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
+                const uint32_t r = seg::tok_get<kHash>(p, tab, key);
+                const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
+                m |= (uint32_t)hit << k;
+                const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
+                if (k & 1) v[h] |= t << 16; else v[h] = t;
+            }
         }
         const uint32_t ident = m == 0xFFFFu;
         const uint32_t M1 = merges_for(m, 1u), M0 = merges_for(m, 0u);
@@ -2875,8 +2908,8 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         const uint32_t ncnt = s_cnt;
         if (ncnt != n) {   // uniform: something merged
             if (vmask) seg::stage_b16(v, L, seg::lds_addr(&s_tok[cur ^ 1][0]) + 2u * lane_off);
-            // chunk starts in [pos0, pos0 + 16) land: their new positions
-            if (nc > 1) {
+            // chunk starts in [pos0, pos0 + 16) land: their new positions (none past n)
+            if (nc > 1 && wave_on) {
                 for (uint32_t a = a_lo > 0 ? a_lo - 1 : 0; a < nc; ++a) {
                     const uint32_t b = s_cpos[cur][a];
                     if (b >= pos0 + 16u) break;
