@@ -806,7 +806,6 @@ constexpr int kS = 2;                                  // sub-tiles per tile
 // cfg5 0.815-0.818 -> 0.804 ms (config_rates, same box); cfg2's 100 MiB, replayed back to back,
 // loses its cache residency (0.0937 -> 0.0955 ms).
 constexpr int kLdPol = 2, kStPol = 2;
-constexpr int kCohPol = 16;   // sc1: a load coherent with other CUs' stores (as an agent-scope atomic load)
 constexpr uint32_t kWavePos = 64u * 16u;               // positions per wave per sub-tile
 constexpr uint64_t kSubPos = (uint64_t)kWaves * kWavePos;
 constexpr int kGroups = kS * kWaves;
@@ -1944,44 +1943,17 @@ __device__ __forceinline__ uint64_t cm_word(const uint64_t* cs, uint64_t nc, uin
 constexpr uint32_t kCmLds = 1024;
 __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     __shared__ uint64_t s_cs[kCmLds];
-    const uint64_t nc = p.nchunks;
-    const bool in_lds = nc <= kCmLds;
-    // the chunk starts are read first, in flight with the pass's two control words below (one
-    // round trip instead of two; a pass that is done reads them for nothing)
-    // the two control words as device-coherent (sc1) buffer loads, without branches around them (an
-    // absent word is a zero-length resource: it reads 0); relaxed atomic loads here each got a
-    // wait of their own
-    // (an offset the compiler cannot see is 0 keeps the words in vector registers: a uniform load
-    // result is moved to a scalar register right after the load, which waits for it there)
-    int z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    const auto nv = __builtin_amdgcn_raw_buffer_load_b64(rsrc_at(p.n_dev, p.n_dev ? 8u : 0u), z, 0, kCohPol);
-    const uint32_t dw = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc_at(p.done, p.done ? 4u : 0u), z, 0, kCohPol);
-    const uint64_t nw = __builtin_bit_cast(uint64_t, nv);
-    constexpr int kPer = (int)(kCmLds / 256u);
-    uint64_t pre[kPer];
-#pragma unroll
-    for (int q = 0; q < kPer; ++q) {   // (cstart holds nc + 1 entries: every index here is valid)
-        const uint64_t i = threadIdx.x + 256u * (uint32_t)q;
-        pre[q] = p.cstart[i < nc ? i : nc];
-    }
-    // every load above issued before the first wait (the scheduler otherwise tests each control word
-    // right after its load)
-    __builtin_amdgcn_sched_barrier(0);
-    const bool done = p.done && dw != 0u;
-    const uint64_t n = p.n_dev ? nw : p.n;
-    // (the exit tests every load, so none is sunk below it: neither n nor a chunk start is ~0)
-    if (done || n == ~0ull || pre[0] == ~0ull) return;
+    const bool done = pass_done(p);      // (both loads in flight together)
+    const uint64_t n = token_count(p);
+    if (done) return;
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
     if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
+    const uint64_t nc = p.nchunks;
+    const bool in_lds = nc <= kCmLds;
     if ((uint64_t)blockIdx.x * 256u * kWavePos >= n) return;   // uniform: no range of this block is live
     if (in_lds) {
-#pragma unroll
-        for (int q = 0; q < kPer; ++q) {
-            const uint32_t i = threadIdx.x + 256u * (uint32_t)q;
-            if (i < nc) s_cs[i] = pre[q];
-        }
+        for (uint32_t i = threadIdx.x; i < nc; i += 256u) s_cs[i] = p.cstart[i];
         __syncthreads();
     }
     const uint64_t lo = r * kWavePos, hi = lo + kWavePos;
@@ -2812,10 +2784,22 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     const uint64_t ngroups = (p.nchunks + grp - 1) / grp;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kFinThreads / 64;
-    if constexpr (kHash != 0) {
+    if constexpr (kHash != 0) {   // four loads in flight per thread per round (not one)
         const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
         uint4* dst = reinterpret_cast<uint4*>(s_fhash);
-        for (uint32_t i = tid; i < p.hbytes / 16u; i += kFinThreads) dst[i] = src[i];
+        const uint32_t nu = p.hbytes / 16u;
+        for (uint32_t i0 = 0; i0 < nu; i0 += 4u * kFinThreads) {
+            // (indices clamped to the last unit, loads and stores unconditional: a branch per load
+            // let the compiler sink each load to its store and wait for it there; the lanes past the
+            // end copy the last unit again, the same bytes)
+            uint4 v0, v1, v2, v3;
+            const uint32_t b = i0 + (uint32_t)tid, last = nu - 1u;
+            const uint32_t j0 = b < nu ? b : last, j1 = b + kFinThreads < nu ? b + kFinThreads : last;
+            const uint32_t j2 = b + 2u * kFinThreads < nu ? b + 2u * kFinThreads : last;
+            const uint32_t j3 = b + 3u * kFinThreads < nu ? b + 3u * kFinThreads : last;
+            v0 = src[j0]; v1 = src[j1]; v2 = src[j2]; v3 = src[j3];
+            dst[j0] = v0; dst[j1] = v1; dst[j2] = v2; dst[j3] = v3;
+        }
     }
     // persistent: groups from the ticket, in order, until none is left
     for (;;) {
@@ -2830,7 +2814,21 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     uint32_t n = (uint32_t)(p.cstart[c1] - S);   // <= kFinCap (the gate)
     const uint16_t* in = reinterpret_cast<const uint16_t*>(p.in);
     for (uint32_t i = tid; i <= nc; i += kFinThreads) s_cpos[0][i] = (uint32_t)(p.cstart[c0 + i] - S);
-    for (uint32_t i = tid; i < kFinCap + 16; i += kFinThreads) s_tok[0][i] = i < n ? in[S + i] : (uint16_t)0;
+    {   // every load in flight before the first LDS store (a rolled loop waited for each: one
+        // global round trip per iteration, 17 of them)
+        constexpr uint32_t kPer = (kFinCap + 16 + kFinThreads - 1) / kFinThreads;
+        uint16_t t[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t i = (uint32_t)tid + q * kFinThreads;
+            t[q] = i < n ? in[S + i] : (uint16_t)0;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t i = (uint32_t)tid + q * kFinThreads;
+            if (i < kFinCap + 16) s_tok[0][i] = t[q];
+        }
+    }
     const uint32_t tab = kHash != 0 ? seg::lds_addr(s_fhash) : 0u;
     __syncthreads();
 
