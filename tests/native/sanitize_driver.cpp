@@ -168,7 +168,8 @@ static void check_device() {
             for (auto& c : in) c = rng() % alph;
             std::vector<uint8_t> out(2 * n + 2);
             size_t len = 0;
-            CHECK(blt_bpe_process_chunk(h, in.data(), n, out.data(), out.size(), &len) == 0, "process_chunk %zu", n);
+            const int prc = blt_bpe_process_chunk(h, in.data(), n, out.data(), out.size(), &len);
+            CHECK(prc == 0, "process_chunk %zu: rc %d, %s", n, prc, prc ? blt_last_error() : "");
             out.resize(len);
             CHECK(out == oracle_chunk(m, in), "process_chunk %zu bytes, trial %d", n, trial);
             for (size_t cs : {4096ul, 65537ul}) {
