@@ -47,7 +47,16 @@ def test_host_checks_under_asan_ubsan():
 
 @pytest.mark.gpu
 def test_device_checks_under_asan_ubsan():
-    r = subprocess.run([_driver()], capture_output=True, text=True, env=ENV, timeout=300)
+    # Under ASan the HIP runtime's start-up fails in some processes (its address-space reservations
+    # and ASan's shadow mappings collide, by layout): the driver then reports "no HIP device" and
+    # runs the host checks only.  A fresh process gets a fresh layout; three tries, then a skip
+    # that says so (the device checks themselves run without ASan in every other GPU test).
+    for _ in range(3):
+        r = subprocess.run([_driver()], capture_output=True, text=True, env=ENV, timeout=300)
+        if "no HIP device" not in r.stdout:
+            break
+    else:
+        pytest.skip("HIP runtime did not start under ASan in three processes: " + r.stdout.splitlines()[0])
     # the first failures name the cause (later ones follow from it): the head of the report too
-    assert r.returncode == 0, r.stdout[:2500] + "\n...\n" + r.stdout[-1500:] + r.stderr[-3000:]
+    assert r.returncode == 0, r.stdout[-1500:] + r.stderr[:2500] + "\n...\n" + r.stderr[-1500:]
     assert "host and device checks: 0 failure(s)" in r.stdout, r.stdout
