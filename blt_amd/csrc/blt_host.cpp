@@ -902,6 +902,20 @@ struct SparseHostLease {
 // counters and the chain block.  Passes went on past four: more batches, one read each, then the
 // compaction (the caller reads the totals).  Nothing changes when the gate word (done and fallback
 // words) is set or detect's seeds overflow the lists (not taken).
+// One sparse batch at a time per device.  sparse_list_kernel and sparse_move_kernel wait for
+// lower-numbered workgroups (workgroups run in blockIdx order on each XCD, which makes that safe for
+// one such kernel on the device); two of them on different streams can each fill an XCD with
+// waiters whose predecessors sit behind the other's (measured: 8 threads of the ASan driver,
+// every wait timing out).  A batch takes the device's lock, waits (on the host) for the previous
+// batch's kernels when they ran on another stream, enqueues its own and records an event after
+// them: no two batches' kernels overlap, and a lone caller (one stream) never waits.
+struct SparseDevLock {
+    std::mutex mu;
+    hipEvent_t last = nullptr;        // after the last batch's kernels
+    hipStream_t last_stream = nullptr;
+};
+SparseDevLock g_sparse_dev[kMaxDevices];
+
 int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
                uint8_t* d_out, const uint64_t* n_dev, uint64_t n_max, const uint64_t* gate, uint64_t k,
                const uint64_t* off_in, uint64_t* off_out, uint64_t* tot, SparseRun* r) {
@@ -909,7 +923,19 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     SparseHostLease lease(h);
     SparseHost* hb = lease.p;
     if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
-    (void)dev;
+    if (dev < 0 || dev >= kMaxDevices) return fail(BLT_E_NODEV, "device index %d out of range", dev);
+    SparseDevLock& dl = g_sparse_dev[dev];
+    std::lock_guard<std::mutex> lk(dl.mu);
+    if (dl.last && dl.last_stream != s) HIP_TRY(hipEventSynchronize(dl.last));
+    if (!dl.last) HIP_TRY(hipEventCreateWithFlags(&dl.last, hipEventDisableTiming));
+    struct Mark {   // the event after this batch's kernels (every return path, errors included)
+        SparseDevLock& dl;
+        hipStream_t s;
+        ~Mark() {
+            if (hipEventRecord(dl.last, s) == hipSuccess) dl.last_stream = s;
+            else (void)hipStreamSynchronize(s), dl.last_stream = s;
+        }
+    } mark{dl, s};
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
     blt::SparseParams q{};
     q.tok = reinterpret_cast<uint16_t*>(d_out);
