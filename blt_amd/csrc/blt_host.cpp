@@ -904,9 +904,10 @@ struct SparseHostLease {
 // words) is set or detect's seeds overflow the lists (not taken).
 // One sparse batch at a time per device.  sparse_list_kernel and sparse_move_kernel wait for
 // lower-numbered workgroups (workgroups run in blockIdx order on each XCD, which makes that safe for
-// one such kernel on the device); two of them on different streams can each fill an XCD with
-// waiters whose predecessors sit behind the other's (measured: 8 threads of the ASan driver,
-// every wait timing out).  A batch takes the device's lock, waits (on the host) for the previous
+// one such kernel on the device); two of them on different streams could each fill an XCD with
+// waiters whose predecessors sit behind the other's (the dispatch order interleaves XCDs, so a
+// later workgroup of one kernel can be resident while an earlier one waits for an XCD the other
+// kernel holds).  A batch takes the device's lock, waits (on the host) for the previous
 // batch's kernels when they ran on another stream, enqueues its own and records an event after
 // them: no two batches' kernels overlap, and a lone caller (one stream) never waits.
 struct SparseDevLock {

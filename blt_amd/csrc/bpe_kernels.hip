@@ -2784,22 +2784,10 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     const uint64_t ngroups = (p.nchunks + grp - 1) / grp;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kFinThreads / 64;
-    if constexpr (kHash != 0) {   // four loads in flight per thread per round (not one)
+    if constexpr (kHash != 0) {
         const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
         uint4* dst = reinterpret_cast<uint4*>(s_fhash);
-        const uint32_t nu = p.hbytes / 16u;
-        for (uint32_t i0 = 0; i0 < nu; i0 += 4u * kFinThreads) {
-            // (indices clamped to the last unit, loads and stores unconditional: a branch per load
-            // let the compiler sink each load to its store and wait for it there; the lanes past the
-            // end copy the last unit again, the same bytes)
-            uint4 v0, v1, v2, v3;
-            const uint32_t b = i0 + (uint32_t)tid, last = nu - 1u;
-            const uint32_t j0 = b < nu ? b : last, j1 = b + kFinThreads < nu ? b + kFinThreads : last;
-            const uint32_t j2 = b + 2u * kFinThreads < nu ? b + 2u * kFinThreads : last;
-            const uint32_t j3 = b + 3u * kFinThreads < nu ? b + 3u * kFinThreads : last;
-            v0 = src[j0]; v1 = src[j1]; v2 = src[j2]; v3 = src[j3];
-            dst[j0] = v0; dst[j1] = v1; dst[j2] = v2; dst[j3] = v3;
-        }
+        for (uint32_t i = tid; i < p.hbytes / 16u; i += kFinThreads) dst[i] = src[i];
     }
     // persistent: groups from the ticket, in order, until none is left
     for (;;) {
@@ -2814,21 +2802,7 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     uint32_t n = (uint32_t)(p.cstart[c1] - S);   // <= kFinCap (the gate)
     const uint16_t* in = reinterpret_cast<const uint16_t*>(p.in);
     for (uint32_t i = tid; i <= nc; i += kFinThreads) s_cpos[0][i] = (uint32_t)(p.cstart[c0 + i] - S);
-    {   // every load in flight before the first LDS store (a rolled loop waited for each: one
-        // global round trip per iteration, 17 of them)
-        constexpr uint32_t kPer = (kFinCap + 16 + kFinThreads - 1) / kFinThreads;
-        uint16_t t[kPer];
-#pragma unroll
-        for (uint32_t q = 0; q < kPer; ++q) {
-            const uint32_t i = (uint32_t)tid + q * kFinThreads;
-            t[q] = i < n ? in[S + i] : (uint16_t)0;
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kPer; ++q) {
-            const uint32_t i = (uint32_t)tid + q * kFinThreads;
-            if (i < kFinCap + 16) s_tok[0][i] = t[q];
-        }
-    }
+    for (uint32_t i = tid; i < kFinCap + 16; i += kFinThreads) s_tok[0][i] = i < n ? in[S + i] : (uint16_t)0;
     const uint32_t tab = kHash != 0 ? seg::lds_addr(s_fhash) : 0u;
     __syncthreads();
 
@@ -2847,11 +2821,8 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         const int32_t rr = (int32_t)n - (int32_t)pos0;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
         uint32_t pairs = (vmask >> 1) | (rr > 16 ? 0x8000u : 0u);
-        // a wave past the group's tokens (uniform: its first position >= n) looks nothing up: the
-        // passes of a chain halve n, so most waves are idle in the later passes
-        const bool wave_on = 1024u * (uint32_t)wave < n;
         uint32_t a_lo = 0;   // first chunk start >= pos0 + 1 (index into s_cpos)
-        if (nc > 1 && wave_on) {
+        if (nc > 1) {
             uint32_t lo = 0, hi = nc;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -2864,18 +2835,16 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
                 pairs &= ~(1u << (b - 1u - pos0));
             }
         }
-        uint32_t v[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, m = 0;
-        if (wave_on) {
+        uint32_t v[8], m = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int h = k >> 1;
-                const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
-                const uint32_t r = seg::tok_get<kHash>(p, tab, key);
-                const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
-                m |= (uint32_t)hit << k;
-                const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
-                if (k & 1) v[h] |= t << 16; else v[h] = t;
-            }
+        for (int k = 0; k < 16; ++k) {
+            const int h = k >> 1;
+            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
+            const uint32_t r = seg::tok_get<kHash>(p, tab, key);
+            const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
+            m |= (uint32_t)hit << k;
+            const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
+            if (k & 1) v[h] |= t << 16; else v[h] = t;
         }
         const uint32_t ident = m == 0xFFFFu;
         const uint32_t M1 = merges_for(m, 1u), M0 = merges_for(m, 0u);
@@ -2906,8 +2875,8 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         const uint32_t ncnt = s_cnt;
         if (ncnt != n) {   // uniform: something merged
             if (vmask) seg::stage_b16(v, L, seg::lds_addr(&s_tok[cur ^ 1][0]) + 2u * lane_off);
-            // chunk starts in [pos0, pos0 + 16) land: their new positions (none past n)
-            if (nc > 1 && wave_on) {
+            // chunk starts in [pos0, pos0 + 16) land: their new positions
+            if (nc > 1) {
                 for (uint32_t a = a_lo > 0 ? a_lo - 1 : 0; a < nc; ++a) {
                     const uint32_t b = s_cpos[cur][a];
                     if (b >= pos0 + 16u) break;

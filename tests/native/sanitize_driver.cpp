@@ -177,8 +177,8 @@ static void check_device() {
                 std::vector<uint64_t> lens((n + cs - 1) / cs + 1);
                 std::vector<size_t> elens(lens.size());
                 size_t gl = 0;
-                CHECK(blt_bpe_process_chunks(h, in.data(), n, cs, 2, got.data(), got.size(), &gl, lens.data()) == 0,
-                      "process_chunks");
+                const int crc = blt_bpe_process_chunks(h, in.data(), n, cs, 2, got.data(), got.size(), &gl, lens.data());
+                CHECK(crc == 0, "process_chunks %zu cs %zu: rc %d, %s", n, cs, crc, crc ? blt_last_error() : "");
                 const size_t el = oracle_run_chunks(m, 0, in.data(), n, cs, -1, 2, exp.data(), elens.data());
                 CHECK(gl == el && memcmp(got.data(), exp.data(), gl) == 0, "process_chunks %zu cs %zu", n, cs);
             }

@@ -573,6 +573,62 @@ def test_concurrent_calls_share_one_handle():
     assert not errors, errors
 
 
+def test_concurrent_sparse_passes():
+    """Round 5: 8 host threads encode with cyclic maps at once (process_chunk, and process_chunks
+    over two contexts on the device), so sparse passes run on several streams.  sparse_list_kernel
+    and sparse_move_kernel wait for lower-numbered workgroups; two of them side by side could starve
+    each other, so run_sparse takes one batch at a time per device.  Every result bit-exact."""
+    import threading
+    rng = np.random.default_rng(31)
+    maps = [synth.SELF_VALUED_MAP]
+    for t in range(3):   # random cyclic maps (values made from themselves) over a small alphabet
+        m = {}
+        for i, (a, b) in enumerate(rng.integers(97, 105, (12, 2))):
+            m.setdefault((int(a), int(b)), int(rng.integers(97, 105)) if i % 2 else 256 + i)
+        for i in range(10):
+            m.setdefault((int(rng.integers(256, 268)), int(rng.integers(97, 105))), int(rng.integers(97, 105)))
+        maps.append(m)
+    strategies = [blt_amd.BpeStrategy(m) for m in maps]
+    oracles = [O.COracle(m) for m in maps]
+    jobs = []
+    for t in range(8):
+        for k in range(4):
+            mi = (t + k) % len(maps)
+            n = int(rng.integers(70_000, 1 << 20))
+            data = synth.text(n, seed=100 + 8 * t + k) if mi == 0 else rng.integers(97, 105, n, dtype=np.uint8)
+            jobs.append((t, k, mi, data, int(rng.choice([4096, 65537, 1 << 18]))))
+    errors = []
+    prev = _sparse(1)
+
+    def worker(t):
+        try:
+            for (tt, k, mi, data, cs) in jobs:
+                if tt != t:
+                    continue
+                s, orc = strategies[mi], oracles[mi]
+                if k % 2:
+                    got = np.frombuffer(s.process_chunk(data.tobytes()), np.uint8)
+                    exp = np.frombuffer(orc.process_chunk(data.tobytes()), np.uint8)
+                else:
+                    got = s.process_chunks(data, cs, n_gpus=2)
+                    exp = orc.run(data, cs, threads=2)
+                if not np.array_equal(got, exp):
+                    errors.append((t, k, mi, data.size, cs))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    try:
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join(timeout=100)
+        assert not any(th.is_alive() for th in threads)
+    finally:
+        _sparse(prev)
+    assert not errors, errors
+
+
 @pytest.mark.parametrize("cs", [1, 2, 3, 7, 16, 17, 1000, 2047])
 def test_tiny_chunk_sizes(cs):
     """The library takes any chunk size > 0 (the CLI clamps to >= 256 KiB, chunking.rs:26-62):
