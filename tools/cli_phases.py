@@ -3,6 +3,7 @@ and the BLT_CLI_TIMING stamps (exec -> main, merges loaded, mmap, HIP runtime up
 windows, writer waits, output closed), plus the HIP start-up probe (build/hip_init_probe).
 
     python tools/cli_phases.py [--mib 1024] [--runs 4] [--out profiles/r04_cli_phases.json]
+    python tools/cli_phases.py --variants ";BLT_PREALLOC_AT=1" --runs 8   (A/B: runs alternate)
 """
 import argparse
 import json
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--runs", type=int, default=4)
     ap.add_argument("--out", default="")
     ap.add_argument("--env", default="", help="extra environment for the CLI, NAME=VALUE[,NAME=VALUE]")
+    ap.add_argument("--variants", default=None,
+                    help="';'-separated environments (NAME=VALUE[,NAME=VALUE], empty = default) run in turn")
     a = ap.parse_args()
     from blt_amd import synth
     base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
@@ -36,20 +39,44 @@ def main():
         if os.path.exists(probe):
             res["hip_init_probe"] = json.loads(subprocess.run([probe], capture_output=True, text=True,
                                                               timeout=60).stdout.strip().splitlines()[-1])
-        env = dict(os.environ, BLT_CLI_TIMING="1")
-        for kv in filter(None, a.env.split(",")):
-            k, v = kv.split("=", 1)
-            env[k] = v
+        def env_of(spec):
+            env = dict(os.environ, BLT_CLI_TIMING="1")
+            for kv in filter(None, spec.split(",")):
+                k, v = kv.split("=", 1)
+                env[k] = v
+            return env
         cmd = [os.path.join(ROOT, "blt_amd", "blt"), "-i", fin, "-o", fout, "--merges", fm, "--chunksize", "16MB",
                "--type", "text", "--gpus", "1"]
-        for _ in range(a.runs):
+
+        def run(env):
             if os.path.exists(fout):
                 os.remove(fout)
             t0 = time.perf_counter()
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env)
             dt = time.perf_counter() - t0
-            res["runs"].append({"wall_s": round(dt, 4), "GBps": round((a.mib << 20) / dt / 1e9, 3), "rc": p.returncode,
-                                "stamps": [ln for ln in p.stderr.splitlines() if ln.startswith("blt timing")]})
+            return dt, p
+        if a.variants is None:
+            env = env_of(a.env)
+            for _ in range(a.runs):
+                dt, p = run(env)
+                res["runs"].append({"wall_s": round(dt, 4), "GBps": round((a.mib << 20) / dt / 1e9, 3), "rc": p.returncode,
+                                    "stamps": [ln for ln in p.stderr.splitlines() if ln.startswith("blt timing")]})
+        else:
+            from bench import cli_phases
+            specs = a.variants.split(";")
+            run(env_of(""))   # warm (page cache of the binary and libraries)
+            res["variants"] = {sp or "default": {"wall_s": [], "phases": [], "rc": []} for sp in specs}
+            for _ in range(a.runs):
+                for sp in specs:
+                    dt, p = run(env_of(sp))
+                    r = res["variants"][sp or "default"]
+                    r["wall_s"].append(round(dt, 4))
+                    r["rc"].append(p.returncode)
+                    r["phases"].append(cli_phases(p.stderr, dt))
+                    print(sp or "default", round(dt, 4), flush=True)
+            for r in res["variants"].values():
+                w = sorted(r["wall_s"])
+                r["median_s"], r["best_s"] = w[len(w) // 2], w[0]
     finally:
         for f in (fin, fout, fm):
             if os.path.exists(f):
