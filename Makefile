@@ -47,7 +47,7 @@ clean:
 .PHONY: all clean
 
 # The timing build of the product kernel (per-wave phase stamps; tools/tile_timing.py with
-# BLT_LIB_PATH=build/exp/libblt_bpe_timing.so).  Experiment variants: tools/build_variant.sh.
+# BLT_LIB_PATH=build/xp/libblt_bpe_timing.so).  Experiment variants: tools/build_variant.sh.
 timing:
 	bash tools/build_variant.sh timing -DBLT_TIMING
 .PHONY: timing

@@ -587,6 +587,8 @@ int sticky_check(const blt_bpe* h) {
 
 // Test hook: per-tile look-back records (blt_debug_set_tile_record).
 uint64_t* g_debug_tiles = nullptr;
+// Test hook (blt_debug_set_inject): blt::kInject* bits, counts the kernels break on purpose.
+std::atomic<uint32_t> g_inject{0};
 // Test hook: n_gpus contexts even where they share a device (blt_debug_set_shared_contexts).
 std::atomic<int> g_shared_contexts{0};
 // Passes 1 and 2 of eligible general maps in one kernel (blt_debug_set_fused(0): the two-kernel
@@ -679,8 +681,8 @@ int ctl_error(const uint32_t* ctl) {
         return fail(BLT_E_IO,
                     "merge-scan device check failed (flags 0x%x: 1 look-back timeout, 2 output range, 4 prefix "
                     "invariant, 8 workgroup wait timeout, 16 chunk map, 32 workspace not zeroed for this size "
-                    "(BLT_ENCODE_WORKSPACE_ZEROED past the last reset); first at tile %u sub-tile %u, O=%llu, "
-                    "value=%llu, C=%u)",
+                    "(BLT_ENCODE_WORKSPACE_ZEROED past the last reset), 64 finish-kernel count invariant; first "
+                    "at tile %u sub-tile %u, O=%llu, value=%llu, C=%u)",
                     ctl[1], ctl[2] ? ctl[2] - 1 : 0, ctl[3], (unsigned long long)ctl[4] | ((unsigned long long)ctl[5] << 32),
                     (unsigned long long)ctl[6] | ((unsigned long long)ctl[7] << 32), ctl[8]);
     return 0;
@@ -748,6 +750,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.allm = h->allmerge ? 1u : 0u;
     p.mark = h->mark | (h->mark << 16);
     p.debug = g_debug_tiles;
+    p.inject = g_inject.load(std::memory_order_relaxed);
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
     p.ws_check = (ws_zeroed && !in_u16 && !chain) ? 1u : 0u;   // the caller's BLT_ENCODE_WORKSPACE_ZEROED
@@ -786,6 +789,7 @@ int run_fused(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint
     p.hone = h->hone ? 1u : 0u;
     p.cs_magic = ~0ull / cs;
     p.debug = g_debug_tiles;
+    p.inject = g_inject.load(std::memory_order_relaxed);
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.fused_fail = fused_fail;
     HIP_TRY(blt::launch_scan_fused(p, dev, s));
@@ -819,6 +823,7 @@ int run_finish(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     p.sticky = h->sticky.load(std::memory_order_acquire);
     p.fin_gate = reinterpret_cast<uint32_t*>(ws + L.total + 32);
     p.debug = g_debug_tiles;
+    p.inject = g_inject.load(std::memory_order_relaxed);
     HIP_TRY(blt::launch_finish(p, dev, s));
     return 0;
 }
@@ -967,6 +972,7 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     q.sample = reinterpret_cast<uint32_t*>(ws + L.sp_ctr + up16(4ull * kSparseCtrWords));
     q.ctl = reinterpret_cast<uint32_t*>(ws + L.ctl);
     q.sticky = h->sticky.load(std::memory_order_acquire);
+    q.inject = g_inject.load(std::memory_order_relaxed);
     uint32_t* seeds[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_seeds0), reinterpret_cast<uint32_t*>(ws + L.sp_seeds1)};
     uint32_t* bits0 = reinterpret_cast<uint32_t*>(ws + L.sp_bits0);
     uint32_t* bits[2] = {reinterpret_cast<uint32_t*>(ws + L.sp_bits1), reinterpret_cast<uint32_t*>(ws + L.sp_bits2)};
@@ -1998,6 +2004,9 @@ uint64_t blt_debug_available_cpus(const char* cgroup_root, const char* proc_cgro
 // Not in the public header: a test hook that makes every merge pass record, per tile, its
 // carry-in/offset/look-back lane and both hypothesis counts into a device buffer.
 void blt_debug_set_tile_record(uint64_t* d_buf) { g_debug_tiles = d_buf; }
+// Not in the public header: blt::kInject* bits (1 finish kernel, 2 u16 scan, 4 sparse move) the next
+// launches break a count with, to check the kernels' invariant checks (returns the old bits).
+uint32_t blt_debug_set_inject(uint32_t bits) { return g_inject.exchange(bits); }
 
 // Not in the public header: the number of u16 passes the calling thread's last general-map
 // encode ran (the pass after which nothing can merge; later enqueued passes returned at once).

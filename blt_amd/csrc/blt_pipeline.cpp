@@ -49,15 +49,22 @@ int set_error(int code, const char* fmt, ...);
 using blt_internal::set_error;
 
 // ---- logging (the reference's tracing, src/main.rs:83-85) ----------------------------------
-// blt_log_init_from_env sets the level from RUST_LOG (BLT_LOG when unset): a comma list of
-// directives, each "level", "target" or "target=level"; the most verbose level among the directives
-// whose target is a prefix of blt_core's (or that name none) applies; none applicable: errors only
-// (EnvFilter's default).  Before the call (library users other than the CLI, as the Python binding)
-// nothing is logged.  Lines go to stdout with one write(2) each (tracing's fmt subscriber writes to
-// stdout; the run's own stdout writes are unbuffered too, so the order is the order of the calls).
+// blt_log_init_from_env sets one level per target this library logs under (blt_core,
+// blt_core::pipeline, blt_core::tokenizer) from RUST_LOG (BLT_LOG when unset), the way
+// tracing-subscriber 0.3's EnvFilter::from_default_env reads it: a comma list of directives, each
+// "level", "target" (every level of it) or "target=level"; a directive applies to a target that
+// starts with its own (a bare level to every target), and of those that apply the one with the
+// longest target decides (the last such when two are equally long); a target no directive applies
+// to logs nothing; a variable that is unset, empty or holds no valid directive means errors only.
+// An unknown level after '=' makes that directive invalid (ignored).  Before the call (library users
+// other than the CLI, as the Python binding) nothing is logged.  Lines go to stdout with one
+// write(2) each (tracing's fmt subscriber writes to stdout; the run's own stdout writes are
+// unbuffered too, so the order is the order of the calls).
 namespace blt_log {
 enum Level { kOff = 0, kError, kWarn, kInfo, kDebug, kTrace };
-std::atomic<int> g_level{-1};   // -1: not initialised (nothing is logged)
+enum Target { kCore = 0, kPipeline, kTokenizer, kTargets };
+const char* const kTargetNames[kTargets] = {"blt_core", "blt_core::pipeline", "blt_core::tokenizer"};
+std::atomic<int> g_level[kTargets] = {{-1}, {-1}, {-1}};   // -1: not initialised (nothing is logged)
 std::mutex g_mu;
 
 int parse_level(const char* s, size_t n) {
@@ -67,37 +74,53 @@ int parse_level(const char* s, size_t n) {
     return -1;
 }
 
-int level_from(const char* v) {
-    int best = -1;
+// the level of target `t` (kTargetNames) under the directives in v (RUST_LOG's value, nullable)
+int level_for(const char* v, int t) {
+    const std::string name = kTargetNames[t];
+    int valid = 0, level = kOff;
+    long spec = -1;   // the deciding directive's target length so far
     for (const char* d = v; d && *d;) {
         const char* e = strchr(d, ',');
         const size_t n = e ? (size_t)(e - d) : strlen(d);
         std::string dir(d, n);
+        d = e ? e + 1 : nullptr;
         while (!dir.empty() && dir.back() == ' ') dir.pop_back();
         while (!dir.empty() && dir.front() == ' ') dir.erase(dir.begin());
+        if (dir.empty()) continue;
         const size_t eq = dir.find('=');
-        int lv = -1;
+        std::string target;
+        int lv;
         if (eq == std::string::npos) {
             lv = parse_level(dir.data(), dir.size());
-            if (lv < 0 && !dir.empty() && std::string("blt_core::pipeline").compare(0, dir.size(), dir) == 0)
-                lv = kTrace;   // a bare target enables every level of it
+            if (lv < 0) {   // a bare target: every level of it
+                target = dir;
+                lv = kTrace;
+            }
         } else {
-            const std::string target = dir.substr(0, eq);
-            if (std::string("blt_core::pipeline").compare(0, target.size(), target) == 0 ||
-                std::string("blt_core::tokenizer").compare(0, target.size(), target) == 0)
-                lv = parse_level(dir.data() + eq + 1, dir.size() - eq - 1);
+            target = dir.substr(0, eq);
+            lv = parse_level(dir.data() + eq + 1, dir.size() - eq - 1);
+            if (lv < 0) continue;   // invalid: ignored
         }
-        if (lv > best) best = lv;
-        d = e ? e + 1 : nullptr;
+        ++valid;
+        if (name.compare(0, target.size(), target) != 0) continue;   // not a prefix of this target
+        if ((long)target.size() >= spec) {
+            spec = (long)target.size();
+            level = lv;
+        }
     }
-    return best < 0 ? (int)kError : best;
+    return valid ? level : (int)kError;
 }
 
-bool on(int lv) { return g_level.load(std::memory_order_relaxed) >= lv; }
+int target_of(const char* name) {
+    for (int t = 0; t < kTargets; ++t)
+        if (strcmp(name, kTargetNames[t]) == 0) return t;
+    return kCore;
+}
+bool on(int lv, int t) { return g_level[t].load(std::memory_order_relaxed) >= lv; }
 
 // "<UTC time>  LEVEL <spans>: <target>: <message>"
 void emit(int lv, const char* spans, const char* target, const char* fmt, ...) {
-    if (!on(lv)) return;
+    if (!on(lv, target_of(target))) return;
     static const char* names[] = {"", "ERROR", " WARN", " INFO", "DEBUG", "TRACE"};
     timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
@@ -130,7 +153,7 @@ void emit(int lv, const char* spans, const char* target, const char* fmt, ...) {
 extern "C" void blt_log_init_from_env(void) {
     const char* v = getenv("RUST_LOG");
     if (!v) v = getenv("BLT_LOG");
-    blt_log::g_level.store(blt_log::level_from(v), std::memory_order_relaxed);
+    for (int t = 0; t < blt_log::kTargets; ++t) blt_log::g_level[t].store(blt_log::level_for(v, t), std::memory_order_relaxed);
 }
 
 namespace {
@@ -140,7 +163,8 @@ constexpr size_t kStdinReadCap = size_t(2) << 20;   // tokio io::blocking DEFAUL
 // Debug lines of the chunks [k0, k1) of a file input (pipeline.rs:108 per received result; the
 // basic strategy's per-chunk line, tokenizer.rs:113).
 void log_chunks(const std::string& span, bool basic, size_t k0, size_t k1, size_t n, size_t cs) {
-    if (!blt_log::on(blt_log::kDebug)) return;
+    if (!blt_log::on(blt_log::kDebug, blt_log::kPipeline) && !(basic && blt_log::on(blt_log::kDebug, blt_log::kTokenizer)))
+        return;   // (emit checks each line's own target)
     for (size_t k = k0; k < k1; ++k) {
         if (basic) {
             const std::string sp = span + ":process_mmap_chunk_task{task_id=" + std::to_string(k) +
@@ -494,7 +518,7 @@ void populate_behind(const OutMap& om, size_t est, std::vector<std::thread>& th)
 // worker pool tokenises (each call stages its chunk through the GPU; the handle is reentrant), a
 // writer emits results in chunk order.  Any error stops reading and is returned.
 int run_stream(const Strategy& st, int in_fd, size_t cs, size_t threads, Sink& sink, const std::string& span) {
-    const bool dbg = blt_log::on(blt_log::kDebug);
+    const bool dbg = blt_log::on(blt_log::kDebug, blt_log::kPipeline) || blt_log::on(blt_log::kDebug, blt_log::kTokenizer);
     const std::string sp_read = span + ":manage_task_spawning";
     threads = std::max<size_t>(1, threads);
     const size_t nworkers = std::min<size_t>(threads, 16);

@@ -71,7 +71,13 @@ struct PassParams {
     uint64_t* debug;           // optional [ntiles * 8] per-tile record (tests only): [4T..]: O,
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
+    uint32_t inject;           // test hook (kInject*): a count broken on purpose, 0 in production
 };
+// Test hook (blt_debug_set_inject): a kernel breaks one of its counts on purpose, to show that its
+// invariant checks turn the count into a flagged error (BLT_E_IO) and no store lands outside the
+// range the count should have given.  Finish kernel: the first pass's count; u16 scan: a tile's
+// count; sparse move: a tile's count.
+constexpr uint32_t kInjectFinish = 1u, kInjectScanTok = 2u, kInjectSparseMove = 4u;
 
 // Generic pass: byte input with the dense LDS table (maps the byte pass cannot take), or BE u16
 // tokens with the bucket table (p.hbuckets) for the later passes of a general map; output BE.
@@ -156,6 +162,7 @@ struct SparseParams {
                                 // words, written whole by the sample kernel)
     uint4* zero;                // the run's counters, tile counts and status words: zeroed by the
     uint32_t zero16;            // sample kernel (16-byte units), ahead of every other sparse kernel
+    uint32_t inject;            // test hook (kInjectSparseMove), 0 in production
 };
 constexpr uint64_t kSparseTile = 8192;    // positions per compaction tile
 // Region / apply kernels: 256-thread workgroups, one list slice per wave (at most kSparseSlices)

@@ -2217,7 +2217,11 @@ __device__ __forceinline__ void load_fused(const PassParams& p, uint64_t n, uint
         nxt[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rd, (int)(wrel + kWavePos), 0, 0);
         const uint64_t wb = tile0 + wrel;
         x[j][4] = 0u;
-        if (wb >= kHalo)   // uniform
+        // (uniform) only a range that holds bytes reads its halo.  Round 5's intermittent illegal
+        // memory access: this load had no `wb < n` test, so the last tile's empty ranges read 64
+        // bytes up to ~32 KiB past the input; with an input allocation of exactly up16(n) bytes (a
+        // pooled context regrown for n) that ran into unmapped pages.
+        if (wb >= kHalo && wb < n)
             x[j][4] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc_at(in + wb - kHalo, kHalo), lane, 0, 0);
     }
     const uint32_t rn = (uint32_t)(left > 0x7FFFFFFFull ? 0x7FFFFFFFull : left);
@@ -2547,8 +2551,12 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 if (lb) lb_finish<true>(p, Tp, lane, lbs, C, O, how, spins, live);
                 live |= (tfl >> 1) & 1u;   // tiles up to and including Tp
                 if (lane == 0) {
-                    const uint64_t end = O + (C == 1u ? tf3 : tf2);
-                    if (C > 1u || O > (uint64_t)Tp * kTileTok || end > n) {
+                    // (test hook: a broken tile count)
+                    const uint64_t end = O + (C == 1u ? tf3 : tf2) + ((KARG(inject) & kInjectScanTok) ? kTileTok : 0u);
+                    // a tile's tokens end within its own input (and the buffer): in place, a range
+                    // past it would overwrite the next tile's unread input
+                    const uint64_t in_end = (uint64_t)(Tp + 1u) * kTileTok < n ? (uint64_t)(Tp + 1u) * kTileTok : n;
+                    if (C > 1u || O > (uint64_t)Tp * kTileTok || end > in_end) {
                         if (C <= 1u) record_error(p, 4u, Tp, 0xFFu, O, end, C);
                         O = 0; C = 2u;
                     }
@@ -2767,6 +2775,14 @@ __device__ __forceinline__ void fin_lookback(const PassParams& p, uint64_t g, in
     }
 }
 
+// Error bit of the finish kernel's invariants (ctl[1]; first-error record: T = group + 1, j = which
+// check, O = the group's offset or 0, value = the count that broke it).  Each is checked before the
+// write it guards, so a broken count is a flagged BLT_E_IO, never a store outside the group's range:
+//   0xF1 the group's input (from the previous pass's chunk offsets) is longer than LDS holds, or its
+//        chunk offsets are not increasing
+//   0xF2 a pass's count is above its input's, or below half of it (a pass at most halves a chunk)
+//   0xF3 the final chunk offsets are not increasing, or end past the group's count
+constexpr uint32_t kFinBadBit = 64u;
 template <int kHash>
 __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p) {
     extern __shared__ __attribute__((aligned(16))) uint2 s_fhash[];
@@ -2784,11 +2800,23 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     const uint64_t ngroups = (p.nchunks + grp - 1) / grp;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int kW = kFinThreads / 64;
-    if constexpr (kHash != 0) {
+    if constexpr (kHash != 0) {   // four loads in flight per thread per round (not one)
         const uint4* src = reinterpret_cast<const uint4*>(p.hbuckets);
         uint4* dst = reinterpret_cast<uint4*>(s_fhash);
-        for (uint32_t i = tid; i < p.hbytes / 16u; i += kFinThreads) dst[i] = src[i];
+        const uint32_t nu = p.hbytes / 16u;
+        for (uint32_t i0 = 0; i0 < nu; i0 += 4u * kFinThreads) {
+            // (indices clamped to the last unit, loads and stores unconditional: a branch per load
+            // let the compiler sink each load to its store and wait for it there; the lanes past the
+            // end copy the last unit again, the same bytes)
+            const uint32_t b = i0 + (uint32_t)tid, last = nu - 1u;
+            const uint32_t j0 = b < nu ? b : last, j1 = b + kFinThreads < nu ? b + kFinThreads : last;
+            const uint32_t j2 = b + 2u * kFinThreads < nu ? b + 2u * kFinThreads : last;
+            const uint32_t j3 = b + 3u * kFinThreads < nu ? b + 3u * kFinThreads : last;
+            const uint4 v0 = src[j0], v1 = src[j1], v2 = src[j2], v3 = src[j3];
+            dst[j0] = v0; dst[j1] = v1; dst[j2] = v2; dst[j3] = v3;
+        }
     }
+    const bool inject = (KARG(inject) & kInjectFinish) != 0u;   // test hook: a broken pass count
     // persistent: groups from the ticket, in order, until none is left
     for (;;) {
     __syncthreads();
@@ -2799,16 +2827,43 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
     const uint64_t c0 = g * grp, c1 = c0 + grp < p.nchunks ? c0 + grp : p.nchunks;
     const uint32_t nc = (uint32_t)(c1 - c0);
     const uint64_t S = p.cstart[c0];
-    uint32_t n = (uint32_t)(p.cstart[c1] - S);   // <= kFinCap (the gate)
+    const uint64_t nin64 = p.cstart[c1] - S;
+    // the group's input: its chunk offsets increasing, its tokens within LDS (the gate says so; a
+    // count that says otherwise is not trusted with the loads and stores below)
+    bool ok_in = nin64 <= kFinCap;
+    for (uint32_t i = tid; i <= nc; i += kFinThreads) {
+        const uint64_t a = p.cstart[c0 + i] - S;
+        const uint64_t b = i < nc ? p.cstart[c0 + i + 1] - S : nin64;
+        ok_in = ok_in && a <= b && b <= nin64;
+        s_cpos[0][i] = (uint32_t)a;
+    }
+    const uint32_t nin = ok_in ? (uint32_t)nin64 : 0u;
     const uint16_t* in = reinterpret_cast<const uint16_t*>(p.in);
-    for (uint32_t i = tid; i <= nc; i += kFinThreads) s_cpos[0][i] = (uint32_t)(p.cstart[c0 + i] - S);
-    for (uint32_t i = tid; i < kFinCap + 16; i += kFinThreads) s_tok[0][i] = i < n ? in[S + i] : (uint16_t)0;
+    {   // every load in flight before the first LDS store (a rolled loop waited for each: one
+        // global round trip per iteration, 17 of them)
+        constexpr uint32_t kPer = (kFinCap + 16 + kFinThreads - 1) / kFinThreads;
+        uint16_t t[kPer];
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t i = (uint32_t)tid + q * kFinThreads;
+            t[q] = i < nin ? in[S + i] : (uint16_t)0;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+            const uint32_t i = (uint32_t)tid + q * kFinThreads;
+            if (i < kFinCap + 16) s_tok[0][i] = t[q];
+        }
+    }
     const uint32_t tab = kHash != 0 ? seg::lds_addr(s_fhash) : 0u;
-    __syncthreads();
+    uint32_t bad = __syncthreads_or(!ok_in) ? 0xF1u : 0u;   // (uniform)
+    uint32_t n = nin;
 
     uint32_t cur = 0;
     const uint32_t pos0 = 16u * (uint32_t)tid;
-    for (;;) {
+    // a wave past the group's tokens looks nothing up (uniform: its first position >= n; a chain's
+    // passes halve n, so most waves idle in the later passes).  The skip changes nothing else: such a
+    // wave's lanes have no valid position, so every mask below is 0 for them either way.
+    for (bool first = true; !bad; first = false) {
         // one greedy pass over s_tok[cur][0, n) into s_tok[cur ^ 1]
         uint32_t x[8];
         {
@@ -2821,8 +2876,9 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         const int32_t rr = (int32_t)n - (int32_t)pos0;
         const uint32_t vmask = rr >= 16 ? 0xFFFFu : (rr <= 0 ? 0u : ((1u << rr) - 1u));
         uint32_t pairs = (vmask >> 1) | (rr > 16 ? 0x8000u : 0u);
+        const bool wave_on = 1024u * (uint32_t)wave < n;
         uint32_t a_lo = 0;   // first chunk start >= pos0 + 1 (index into s_cpos)
-        if (nc > 1) {
+        if (nc > 1 && wave_on) {
             uint32_t lo = 0, hi = nc;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -2835,16 +2891,18 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
                 pairs &= ~(1u << (b - 1u - pos0));
             }
         }
-        uint32_t v[8], m = 0;
+        uint32_t v[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u}, m = 0;
+        if (wave_on) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int h = k >> 1;
-            const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
-            const uint32_t r = seg::tok_get<kHash>(p, tab, key);
-            const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
-            m |= (uint32_t)hit << k;
-            const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
-            if (k & 1) v[h] |= t << 16; else v[h] = t;
+            for (int k = 0; k < 16; ++k) {
+                const int h = k >> 1;
+                const uint32_t key = (k & 1) ? __builtin_amdgcn_alignbyte(h < 7 ? x[h + 1] : nxt, x[h], 2) : x[h];
+                const uint32_t r = seg::tok_get<kHash>(p, tab, key);
+                const bool hit = (r >> 31) != 0u && ((pairs >> k) & 1u);
+                m |= (uint32_t)hit << k;
+                const uint32_t t = hit ? (r & 0xFFFFu) : ((x[h] >> (16 * (k & 1))) & 0xFFFFu);
+                if (k & 1) v[h] |= t << 16; else v[h] = t;
+            }
         }
         const uint32_t ident = m == 0xFFFFu;
         const uint32_t M1 = merges_for(m, 1u), M0 = merges_for(m, 0u);
@@ -2864,19 +2922,25 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
             resolve_wave(gi, gco, g0, g1, lane, ghb, gbc, gex, tf);
             // the group's first token lands (carry-in 1): the high halves
             if (lane < kW) { s_gin[lane][0] = ghb ? gbc : 1u; s_gin[lane][1] = gex >> 16; }
-            if (lane == 0) s_cnt = tf.cnt1;
+            if (lane == 0) s_cnt = tf.cnt1 + (inject && first ? kFinCap : 0u);
         }
         __syncthreads();
+        const uint32_t ncnt = s_cnt;
+        // (uniform) a pass keeps at most its input's tokens and at least half of them: any other
+        // count would place the stage writes and the group's output by wrong offsets
+        if (ncnt > n || 2u * ncnt < n) {
+            bad = 0xF2u;   // (s_cnt keeps the count for the record)
+            break;
+        }
         const uint32_t cg = s_gin[wave][0];
         const uint32_t c = hasb ? bco : cg;
         const uint32_t lane_off = s_gin[wave][1] + (cg ? (excl >> 16) : (excl & 0xFFFFu));
         const uint32_t M = merges_for(m, c);
         const uint32_t L = lands_for(M, c, vmask);
-        const uint32_t ncnt = s_cnt;
         if (ncnt != n) {   // uniform: something merged
             if (vmask) seg::stage_b16(v, L, seg::lds_addr(&s_tok[cur ^ 1][0]) + 2u * lane_off);
-            // chunk starts in [pos0, pos0 + 16) land: their new positions
-            if (nc > 1) {
+            // chunk starts in [pos0, pos0 + 16) land: their new positions (none past n)
+            if (nc > 1 && wave_on) {
                 for (uint32_t a = a_lo > 0 ? a_lo - 1 : 0; a < nc; ++a) {
                     const uint32_t b = s_cpos[cur][a];
                     if (b >= pos0 + 16u) break;
@@ -2891,33 +2955,47 @@ __global__ __launch_bounds__(kFinThreads) void finish_chunks_kernel(PassParams p
         cur ^= 1;
         n = ncnt;
     }
+    if (!bad) {   // the final chunk offsets: increasing, the last one the count
+        bool ok = true;
+        for (uint32_t i = tid; i < nc; i += kFinThreads) ok = ok && s_cpos[cur][i] <= s_cpos[cur][i + 1];
+        if (__syncthreads_or(!ok || s_cpos[cur][nc] != n)) bad = 0xF3u;
+    }
 
     // place the group: its count as an aggregate (constant carry 1: chunks never merge across), the
-    // look-back over the groups before it, then its tokens, chunk offsets and (last group) the total
+    // look-back over the groups before it, then its tokens, chunk offsets and (last group) the total.
+    // A group that broke an invariant flags it and writes nothing; it publishes its input count so
+    // the groups after it still finish (their offsets stay below their own inputs).
     if (wave == 0) {
         uint32_t C = 1u, how = 0, spins = 0;
         uint64_t O = 0;
+        const uint32_t cnt = bad ? (uint32_t)(nin64 < (1ull << 30) ? nin64 : (1ull << 30) - 1u) : n;
         if (g == 0) {
-            if (lane == 0) st_publish(p.status, st_incl(1u, n));
+            if (lane == 0) st_publish(p.status, st_incl(1u, cnt));
         } else {
-            if (lane == 0) st_publish(p.status + g, st_agg(1u, 1u, n, n));
-            fin_lookback(p, g, lane, C, O, how, spins);
-            if (lane == 0) {
-                if (C > 1u || O > S) {   // a failed look-back (flagged) or a broken prefix: write nothing
-                    if (C <= 1u) record_error(p, 4u, (uint32_t)g, 0xFEu, O, n, C);
-                    O = ~0ull;
-                } else {
-                    st_publish(p.status + g, st_incl(1u, O + n));
+            if (lane == 0) st_publish(p.status + g, st_agg(1u, 1u, cnt, cnt));
+            if (!bad) {
+                fin_lookback(p, g, lane, C, O, how, spins);
+                if (lane == 0) {
+                    if (C > 1u || O > S) {   // a failed look-back (flagged) or a broken prefix: write nothing
+                        if (C <= 1u) record_error(p, 4u, (uint32_t)g, 0xFEu, O, n, C);
+                        O = ~0ull;
+                    } else {
+                        st_publish(p.status + g, st_incl(1u, O + n));
+                    }
                 }
             }
+        }
+        if (bad) {
+            if (lane == 0) record_error(p, kFinBadBit, (uint32_t)g, bad, S, bad == 0xF2u ? s_cnt : n, nc);
+            O = ~0ull;
         }
         if (lane == 0) {
             s_O = O;
             if (p.debug) {   // tests only: the group's record
                 uint64_t* d = p.debug + 16ull * g;
-                d[0] = g; d[1] = S; d[2] = p.cstart[c1] - S; d[3] = n; d[4] = O;
+                d[0] = g; d[1] = S; d[2] = nin64; d[3] = n; d[4] = O;
                 d[5] = C | ((uint64_t)how << 8) | ((uint64_t)spins << 32);
-                d[6] = lmax | ((uint64_t)grp << 32); d[7] = nc;
+                d[6] = lmax | ((uint64_t)grp << 32); d[7] = nc | ((uint64_t)bad << 32);
                 d[8] = g ? st_read(p.status + g - 1) : 0; d[9] = st_read(p.status);
                 d[10] = st_read(p.status + g);
                 d[11] = g >= 2 ? st_read(p.status + g - 2) : 0;
@@ -3753,15 +3831,18 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
             }
             lbase += lt;
         }
-        const uint32_t ttot = lbase - e;
+        const uint32_t ttot = lbase - e + ((qa.inject & kInjectSparseMove) ? 1u : 0u);   // (test hook)
         const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
         __syncthreads();   // staged: every load of the tile done
+        // the tile's count against the scan's hole counts (the bitmap against the apply kernels'
+        // counters): a tile whose counts disagree, or whose output would not lie within its own
+        // input, flags error bit 4 and writes nothing
+        const bool counts_ok = ttot == (in_end - tile0) - (hnext - hb) && hb <= tile0 && O + ttot <= in_end;
         if (tid == 0) {
             if (kMoveTiles == 1) st_publish(qa.status + T, kMvRead);
-            if (ttot != (in_end - tile0) - (hnext - hb) || hb > tile0) flag_error(qa.ctl, qa.sticky, 4u);   // counts vs bitmap
+            if (!counts_ok) flag_error(qa.ctl, qa.sticky, 4u);
         }
-        // else in place already; an output range past the tile's input (bad counts) writes nothing
-        const bool moves = !(O == tile0 && ttot == in_end - tile0) && hb <= tile0 && O + ttot <= in_end;
+        const bool moves = counts_ok && !(O == tile0 && ttot == in_end - tile0);   // (else in place already)
         if (!moves) continue;   // (uniform)
         if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
             bool bad = false;
@@ -3774,9 +3855,14 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
-            if (__ballot(bad) != 0ull && lane == 0) flag_error(qa.ctl, qa.sticky, 1u);
+            if (__ballot(bad) != 0ull && lane == 0) {
+                flag_error(qa.ctl, qa.sticky, 1u);
+                s_wsum[0][0] = ~0u;   // (after the barrier below: every wave has read s_wsum)
+            }
         }
         __syncthreads();
+        // a wait that timed out (flagged): the input it waited for may be unread, so nothing is written
+        if (s_wsum[0][0] == ~0u) continue;   // (uniform)
         // output groups r = 0 .. nr - 1 (global tokens 8 (O / 8 + r) ..): whole ones with one 16-byte
         // store, the partial first and last token by token
         const uint32_t nr = (e + ttot + 7u) / 8u;

@@ -246,11 +246,16 @@ int main(int argc, char** argv) {
         blt_bpe_create(&a, &b, &v, 1, 0, &h);
         const int rc = blt_bpe_process_chunk(h, in, 2, out, 4, &len);
         blt_bpe_destroy(h);
-        if (rc != 0) {
+        if (rc == BLT_E_NODEV) {
             // no device, or a HIP runtime that did not come up in this process (under ASan the
             // runtime's start-up fails now and then, as ASan's shadow mappings land where it
             // needs address space): host-only checks, and the message says why
             printf("no HIP device: host-only checks (probe rc %d: %s)\n", rc, blt_last_error());
+            cpu = true;
+        } else if (rc != 0) {
+            // a device that is there but failed the probe (a kernel fault, a sticky error, a broken
+            // launch) is a failure, not a reason to skip the device checks
+            CHECK(false, "device probe: rc %d, %s", rc, blt_last_error());
             cpu = true;
         } else {
             check_device();

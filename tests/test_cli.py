@@ -315,6 +315,19 @@ def test_log_levels_and_messages(tmp_path):
     assert r.returncode == 0 and r.stdout == b""
     r = run(args, env=dict(env, BLT_LOG="warn"))
     assert r.stdout == b""
+    # one level per target, the longest matching directive deciding (EnvFilter): a
+    # tokenizer directive enables no pipeline line, a pipeline directive no blt_core line
+    r = run(args, env=dict(env, RUST_LOG="blt_core::tokenizer=debug"))
+    assert r.returncode == 0 and r.stdout == b""
+    r = run(args, env=dict(env, RUST_LOG="blt_core::pipeline=info"))
+    assert [(lv.strip(), tgt, msg) for lv, _, tgt, msg in _log_lines(r.stdout)] == [
+        ("INFO", "blt_core::pipeline", "Running pipeline in Mmap mode for file of size: 600000")]
+    r = run(args, env=dict(env, RUST_LOG="debug,blt_core::pipeline=info"))
+    lv_tgt = {(lv.strip(), tgt) for lv, _, tgt, _ in _log_lines(r.stdout)}
+    assert ("INFO", "blt_core") in lv_tgt and ("INFO", "blt_core::pipeline") in lv_tgt
+    assert ("DEBUG", "blt_core::pipeline") not in lv_tgt
+    r = run(args, env=dict(env, RUST_LOG="blt_core=verbose"))   # invalid only: errors only
+    assert r.returncode == 0 and r.stdout == b""
     r = run(["--passthrough", "--chunksize", "256KB"], stdin=b"abc", env=dict(env, RUST_LOG="debug"))
     msgs = [msg for _, _, _, msg in _log_lines(r.stdout)]
     assert "Running pipeline in Stream mode for stdin" in msgs

@@ -48,15 +48,19 @@ def test_host_checks_under_asan_ubsan():
 @pytest.mark.gpu
 def test_device_checks_under_asan_ubsan():
     # Under ASan the HIP runtime's start-up fails in some processes (its address-space reservations
-    # and ASan's shadow mappings collide, by layout): the driver then reports "no HIP device" and
-    # runs the host checks only.  A fresh process gets a fresh layout; three tries, then a skip
-    # that says so (the device checks themselves run without ASan in every other GPU test).
-    for _ in range(3):
+    # and ASan's shadow mappings collide, by layout): the driver's probe then gets BLT_E_NODEV, says
+    # "no HIP device" and runs the host checks only.  A fresh process gets a fresh layout: up to five
+    # tries for that one start-up error.  Any other probe failure is a driver failure (the probe
+    # reports it), and so is a runtime that never starts on a box whose GPU the plain suite sees: the
+    # device checks never turn into a skip.
+    import torch
+    for _ in range(5):
         r = subprocess.run([_driver()], capture_output=True, text=True, env=ENV, timeout=300)
         if "no HIP device" not in r.stdout:
             break
     else:
-        pytest.skip("HIP runtime did not start under ASan in three processes: " + r.stdout.splitlines()[0])
+        assert not torch.cuda.is_available(), "HIP runtime did not start under ASan in five processes: " + r.stdout
+        pytest.skip("no GPU")
     # the first failures name the cause (later ones follow from it): the head of the report too
     assert r.returncode == 0, r.stdout[-1500:] + r.stderr[:2500] + "\n...\n" + r.stderr[-1500:]
     assert "host and device checks: 0 failure(s)" in r.stdout, r.stdout

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Builds an experiment variant of the product library: build/exp/libblt_bpe_NAME.so with extra
+# Builds an experiment variant of the product library: build/xp/libblt_bpe_NAME.so (objects in
+# build/exp, which no GPU call ships) with extra
 # compile flags (e.g. -DBLT_PAIRW=1).  Run tests or bench against it with BLT_LIB_PATH.
 #   tools/build_variant.sh pw "-DBLT_PAIRW=1"
 # KFLAGS (environment): extra flags for the kernel source only (e.g. -mllvm scheduler options)
@@ -14,5 +15,5 @@ $HIPCC $HF $FLAGS -x hip -c "$R/blt_amd/csrc/blt_host.cpp" -o "$R/build/exp/h_$N
 $HIPCC $HF $FLAGS -x hip -c "$R/blt_amd/csrc/blt_pipeline.cpp" -o "$R/build/exp/p_$NAME.o" &
 $HIPCC $HF $FLAGS ${KFLAGS:-} -I"$R/blt_amd/csrc" -c "${KSRC:-$R/blt_amd/csrc/bpe_kernels.hip}" -o "$R/build/exp/k_$NAME.o"
 wait
-$HIPCC $HF -shared -o "$R/build/exp/libblt_bpe_$NAME.so" "$R/build/exp/k_$NAME.o" "$R/build/exp/h_$NAME.o" "$R/build/exp/p_$NAME.o" -lpthread
-echo "built build/exp/libblt_bpe_$NAME.so ($FLAGS)"
+mkdir -p "$R/build/xp"; $HIPCC $HF -shared -o "$R/build/xp/libblt_bpe_$NAME.so" "$R/build/exp/k_$NAME.o" "$R/build/exp/h_$NAME.o" "$R/build/exp/p_$NAME.o" -lpthread
+echo "built build/xp/libblt_bpe_$NAME.so ($FLAGS)"

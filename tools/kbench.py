@@ -1,6 +1,6 @@
 """Kernel-only timing of the byte-pass merge scan on cfg2 / cfg3 / cfg5 (one GPU, one library build).
 
-    BLT_LIB_PATH=build/exp/libblt_bpe_X.so python tools/kbench.py [--only cfg3,cfg5] [--check]
+    BLT_LIB_PATH=build/xp/libblt_bpe_X.so python tools/kbench.py [--only cfg3,cfg5] [--check]
 
 Inputs resident in HBM; per config the median of --reps launches timed with HIP events on the
 launch stream, the workspace reset outside the events.  --check compares the output with the

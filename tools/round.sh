@@ -11,9 +11,9 @@
 #   bench              the driver's command: bench.py --gpus 1 --steps 20 --warmup 5, bench.json
 #   bench:ARGS         bench.py with extra arguments (+ for spaces), bench_<n>.json
 #   benche:NAME=VALUE:ARGS  bench.py with one environment setting
-#   benchlib:LIBTAG:ARGS  bench.py on build/exp/libblt_bpe_LIBTAG.so
-#   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/exp/libblt_bpe_LIBTAG.so)
-#   tim:LIBTAG[:ARGS]  tools/tile_timing.py on a timing build (build/exp/libblt_bpe_LIBTAG.so)
+#   benchlib:LIBTAG:ARGS  bench.py on build/xp/libblt_bpe_LIBTAG.so
+#   kbench[:LIBTAG]    tools/kbench.py on cfg2/cfg3/cfg5 (LIBTAG: build/xp/libblt_bpe_LIBTAG.so)
+#   tim:LIBTAG[:ARGS]  tools/tile_timing.py on a timing build (build/xp/libblt_bpe_LIBTAG.so)
 #   prof:WL            rocprofv3 --kernel-trace --stats of bench.py --workload WL (cfg2|cfg3|cfg5)
 #   proff2[:ROWS]      rocprofv3 kernel stats of the f2 rows (bench.py --only-configs ROWS)
 #   pmc:WL[:GROUPS]    tools/pmc_profile.py on bench.py --workload WL (groups default fetch,write,insts)
@@ -61,16 +61,16 @@ for st in "$@"; do
     benchlib)
       # bench.py on an experiment build: benchlib:LIBTAG:ARGS (ARGS + for spaces)
       nb=$((nb + 1))
-      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 400 python bench.py ${b//+/ } > "$O/bench_${a}_$nb.json" 2> "$O/bench_${a}_$nb.err"
+      BLT_LIB_PATH=$R/build/xp/libblt_bpe_$a.so timeout -k 10 400 python bench.py ${b//+/ } > "$O/bench_${a}_$nb.json" 2> "$O/bench_${a}_$nb.err"
       echo "[$a]"; python tools/summarize_bench.py "$O/bench_${a}_$nb.json" ;;
     kbench)
-      lib=""; [ -n "$a" ] && lib="$R/build/exp/libblt_bpe_$a.so"
+      lib=""; [ -n "$a" ] && lib="$R/build/xp/libblt_bpe_$a.so"
       BLT_LIB_PATH=$lib timeout -k 10 300 python tools/kbench.py --check >> "$O/kbench.jsonl" 2> "$O/kbench.err"
       tail -3 "$O/kbench.jsonl" ;;
     tim)
       # per-wave phase timing of a timing build (-DBLT_TIMING): tim:LIBTAG[:ARGS] (ARGS + for spaces)
       nb=$((nb + 1))
-      BLT_LIB_PATH=$R/build/exp/libblt_bpe_$a.so timeout -k 10 300 python tools/tile_timing.py ${b//+/ } \
+      BLT_LIB_PATH=$R/build/xp/libblt_bpe_$a.so timeout -k 10 300 python tools/tile_timing.py ${b//+/ } \
         > "$O/tim_${a}_$nb.txt" 2>&1
       head -22 "$O/tim_${a}_$nb.txt" | grep -E "^256|exit|publishes|wave  0|wave  8|wave 12|spins|rounds" ;;
     prof)

@@ -1,5 +1,5 @@
 """Per-tile phase timing of the byte-pass kernel (s_memtime stamps through the debug hook, in
-the timing build build/exp/libblt_bpe_timing.so from `make exp`, or BLT_LIB_PATH).
+the timing build build/xp/libblt_bpe_timing.so from `make exp`, or BLT_LIB_PATH).
 
     python tools/tile_timing.py [MiB] [--random] [--few]   (--random: cfg5's random bytes instead of cfg3's
     text; --few: a two-merge map, ~1 token per byte)

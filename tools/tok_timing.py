@@ -1,5 +1,5 @@
 """Per-wave phase timing of the u16 scan kernel (general maps) in the timing build
-(build/exp/libblt_bpe_timing.so: tools/build_variant.sh timing -DBLT_TIMING), on the 256 MiB
+(build/xp/libblt_bpe_timing.so: tools/build_variant.sh timing -DBLT_TIMING), on the 256 MiB
 multi-pass case of tools/config_rates.py (chained text map: one byte pass, one u16 pass).
 
     python tools/tok_timing.py [MiB]
