@@ -930,6 +930,21 @@ __device__ __forceinline__ void lane_wave_fns(const uint32_t (&m)[NS], uint32_t 
     for (int j = 0; j < NS; ++j) wnonid[j] = __ballot(m[j] != 0xFFFFu);   // lanes that are not identities
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
+#ifndef BLT_NO_DENSE_FNS
+        if (wnonid[j] == 0) {
+            // (uniform) a dense wave range: every position of every lane merges (and is valid: a
+            // lane with a cut merge or an invalid position is no identity), as on text under a large
+            // merge map.  Every lane is an identity and takes the wave's carry-in; under either it
+            // emits 8 tokens (positions 0, 2, .., 14 or 1, 3, .., 15), so its exclusive count is
+            // 8 lane under both hypotheses and the wave emits 512.  Carry-in bits: 0 under wave
+            // carry-in 0, 1 under 1.  (The general path below derives the same words in ~30 VALU and
+            // ~10 SALU instructions per wave range.)
+            st.ex[j] = (uint32_t)lane * 0x00080008u | 0x80000000u;
+            wcmask[j] = 0;
+            wincl[j] = 0x02000200u;
+            continue;
+        }
+#endif
         const uint32_t vm = st.mv[j] >> 16;
         const uint32_t mc = (m[j] & ~1u) | (m[j] << 16);
         const uint32_t sst = mc & ~pk_shl1(mc);
@@ -1689,7 +1704,8 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
         // LDS-DMA, every load in flight at once (one wave-instruction fills 1 KiB of LDS).  (A
         // rolled copy loop waits for each load: one L2/MALL round trip each, ~0.7 us when all 256
-        // workgroups copy at once, 6.9 us in all.)
+        // workgroups copy at once, 6.9 us in all.  Round 6: the first tile's loads issued beside the
+        // copy, the tickets handed over by an LDS-only barrier, measured cfg2 2 % slower.)
         constexpr int kUnits = (int)(kSelfEntries * 2 / 16);
         constexpr int kPer = (kUnits + kThreads - 1) / kThreads;
 #pragma unroll
