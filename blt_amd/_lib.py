@@ -92,7 +92,6 @@ _DEBUG_SIGNATURES = {
     "blt_debug_inject_device_error": (ctypes.c_int, [_vp, _vp, _vp]),
     "blt_debug_set_tile_record": (None, [_vp]),
     "blt_debug_set_inject": (ctypes.c_uint32, [ctypes.c_uint32]),
-    "blt_debug_set_self_copy": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_last_u16_passes": (ctypes.c_uint32, []),
     "blt_debug_set_shared_contexts": (None, [ctypes.c_int]),
     "blt_debug_set_pin_ring": (ctypes.c_int, [ctypes.c_int]),

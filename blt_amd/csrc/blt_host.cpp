@@ -240,7 +240,6 @@ struct DevTables {
     uint16_t* self_ne = nullptr;    // self-token table, native byte order (byte-pass kernel)
     uint16_t* self_be = nullptr;    // self-token table, output (big-endian) byte order
     uint2* hbuckets = nullptr;      // general map: cuckoo buckets (u16 passes)
-    uint2* self_sparse = nullptr;   // small maps: the self-token table's merge entries (self_list)
 };
 
 struct blt_bpe {
@@ -267,10 +266,6 @@ struct blt_bpe {
     // known up front, so they are enqueued without reading the device's pass count.
     uint32_t chain_depth = 0;
     std::vector<uint16_t> self_ne, self_be;
-    // The entries of self_be that are no self token (BE(a) at (a, b)), as [index, value] pairs, when
-    // there are at most blt::kSelfSparseMax of them (else empty): the byte pass then writes the
-    // table into LDS itself instead of copying 132 KiB (round 6).
-    std::vector<uint32_t> self_list;
     // General map (not single_pass): 2-choice cuckoo table of one-slot buckets for the u16 passes
     // (blt::bucket_of), words [key, val]; key = BE(a) | BE(b) << 16, val = BE(value) | 1 << 31
     // | 1 << 30 when the value is a component of some key.
@@ -498,15 +493,6 @@ int build_handle(const std::vector<uint32_t>& keys, const std::vector<uint16_t>&
     }
     h->self_be.resize(blt::kSelfEntries);
     for (uint32_t i = 0; i < blt::kSelfEntries; ++i) h->self_be[i] = bswap(h->self_ne[i]);
-    for (uint32_t a = 0; a < 256 && h->self_list.size() <= 2 * blt::kSelfSparseMax; ++a)
-        for (uint32_t b = 0; b < 256; ++b) {
-            const uint32_t i = blt::self_index(a, b);
-            if (h->self_be[i] != bswap(a)) {
-                h->self_list.push_back(i);
-                h->self_list.push_back(h->self_be[i]);
-            }
-        }
-    if (h->self_list.size() > 2 * blt::kSelfSparseMax) h->self_list.clear(), h->self_list.push_back(~0u);
     if (!h->single_pass && !build_buckets(map, is_comp, h.get())) return fail(BLT_E_NOMEM, "cannot place the merge map in a hash table");
     *out = h.release();
     return 0;
@@ -542,17 +528,13 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out, hipStream_t via =
         auto up256 = [](size_t x) { return (x + 255) & ~size_t(255); };
         const size_t b_dense = 65536 * sizeof(uint16_t), b_self = blt::kSelfEntries * sizeof(uint16_t);
         const size_t b_hash = h->hwords.size() * sizeof(uint32_t);
-        const bool sparse = h->self_list.size() != 1;   // (one word: too many entries)
-        const size_t b_list = sparse ? h->self_list.size() * sizeof(uint32_t) : 0;
         const size_t o_ne = up256(b_dense), o_be = o_ne + up256(b_self), o_hash = o_be + up256(b_self);
-        const size_t o_list = o_hash + up256(b_hash);
-        const size_t total = o_list + up256(b_list);
+        const size_t total = o_hash + up256(b_hash);
         std::vector<uint8_t> blob(total, 0);
         memcpy(blob.data(), h->dense.data(), b_dense);
         memcpy(blob.data() + o_ne, h->self_ne.data(), b_self);
         memcpy(blob.data() + o_be, h->self_be.data(), b_self);
         if (b_hash) memcpy(blob.data() + o_hash, h->hwords.data(), b_hash);
-        if (b_list) memcpy(blob.data() + o_list, h->self_list.data(), b_list);
         hipStream_t us = via;
         uint8_t* base = nullptr;
         detail_stamp("tables: blob built");
@@ -567,8 +549,6 @@ int device_tables(const blt_bpe* hc, int dev, DevTables** out, hipStream_t via =
             t.self_ne = reinterpret_cast<uint16_t*>(base + o_ne);
             t.self_be = reinterpret_cast<uint16_t*>(base + o_be);
             if (b_hash) t.hbuckets = reinterpret_cast<uint2*>(base + o_hash);
-            // (an empty list is a map with no byte-pair merge: the table is all self tokens)
-            if (sparse) t.self_sparse = reinterpret_cast<uint2*>(base + o_list);
         }
         ok = ok && hipStreamSynchronize(us) == hipSuccess;
         detail_stamp("tables: copied");
@@ -609,8 +589,6 @@ int sticky_check(const blt_bpe* h) {
 uint64_t* g_debug_tiles = nullptr;
 // Test hook (blt_debug_set_inject): blt::kInject* bits, counts the kernels break on purpose.
 std::atomic<uint32_t> g_inject{0};
-// Test hook (blt_debug_set_self_copy): 1 = the byte pass copies its whole table even for small maps.
-std::atomic<int> g_self_copy{0};
 // Test hook: n_gpus contexts even where they share a device (blt_debug_set_shared_contexts).
 std::atomic<int> g_shared_contexts{0};
 // Passes 1 and 2 of eligible general maps in one kernel (blt_debug_set_fused(0): the two-kernel
@@ -758,10 +736,6 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.ntiles = (uint32_t)ntiles;
     p.sentinel = h->sentinel;
     p.dense = columnar ? (be ? t->self_be : t->self_ne) : t->dense;
-    if (columnar && be && t->self_sparse && !g_self_copy.load(std::memory_order_relaxed)) {
-        p.self_sparse = t->self_sparse;
-        p.self_nsparse = (uint32_t)(h->self_list.size() / 2);
-    }
     p.hbuckets = t->hbuckets;
     p.hmul1 = h->hmul1;
     p.hmul2 = h->hmul2;
@@ -2033,9 +2007,6 @@ void blt_debug_set_tile_record(uint64_t* d_buf) { g_debug_tiles = d_buf; }
 // Not in the public header: blt::kInject* bits (1 finish kernel, 2 u16 scan, 4 sparse move) the next
 // launches break a count with, to check the kernels' invariant checks (returns the old bits).
 uint32_t blt_debug_set_inject(uint32_t bits) { return g_inject.exchange(bits); }
-// Not in the public header: 1 = the byte pass copies its 132 KiB table from global memory even for a
-// map with few byte-pair merges (0, the default: such maps' tables are written in LDS).
-int blt_debug_set_self_copy(int on) { return g_self_copy.exchange(on ? 1 : 0); }
 
 // Not in the public header: the number of u16 passes the calling thread's last general-map
 // encode ran (the pass after which nothing can merge; later enqueued passes returned at once).

@@ -72,11 +72,7 @@ struct PassParams {
                                // C|how, counts, carry-outs; byte pass [4 ntiles + 4T..]: s_memtime at
                                // the iteration start, after the first and second barrier; spins
     uint32_t inject;           // test hook (kInject*): a count broken on purpose, 0 in production
-    const uint2* self_sparse;  // byte pass, maps with few byte-pair merges (else null): the self-token
-    uint32_t self_nsparse;     // table's entries that are no self token, [index, value]; the kernel
-                               // writes the table in LDS (self tokens, then these) instead of copying it
 };
-constexpr uint32_t kSelfSparseMax = 4096;   // merge entries up to which the byte pass writes its table
 // Test hook (blt_debug_set_inject): a kernel breaks one of its counts on purpose, to show that its
 // invariant checks turn the count into a flagged error (BLT_E_IO) and no store lands outside the
 // range the count should have given.  Finish kernel: the first pass's count; u16 scan: a tile's

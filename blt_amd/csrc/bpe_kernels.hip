@@ -1699,39 +1699,7 @@ __global__ __launch_bounds__(kThreads) void scan_bytes_kernel(PassParams p) {
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
-    if (const uint2* sl = p.self_sparse) {
-        // (uniform) a map with few byte-pair merges (round 6): the table written here, not copied.
-        // The self tokens first, one 16-byte LDS store per unit (a dword holds two entries of one
-        // row, BE(a) = a << 8 each; row a is dwords [129 a, 129 a + 129), its last the 2-entry pad),
-        // then the merge entries from the host's list, whose loads fly during the fill.  132 KiB of
-        // LDS stores and 8 bytes per merge read, against 132 KiB read from L2/MALL by every
-        // workgroup at once (cfg2's 256 merges: the copy took a workgroup 5.7 us).
-        constexpr uint32_t kPerL = kSelfSparseMax / kThreads;
-        const uint32_t ns = p.self_nsparse;
-        uint2 e[kPerL];
-#pragma unroll
-        for (uint32_t q = 0; q < kPerL; ++q) {
-            const uint32_t i = (uint32_t)tid + q * kThreads;
-            e[q] = ns ? sl[i < ns ? i : ns - 1u] : make_uint2(0u, 0u);   // (indices within the list)
-        }
-        constexpr uint32_t kDw = kSelfEntries / 2, kU = kDw / 4;   // 33024 dwords, 8256 units
-        static_assert(kDw % 4 == 0 && kSelfRow == 258, "self-table fill geometry");
-        for (uint32_t u = (uint32_t)tid; u < kU; u += kThreads) {
-            u32x4 w;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t a = __umulhi(4u * u + (uint32_t)k, 33294321u);   // dword / 129 (exact below 33024)
-                w[k] = (a << 8) | (a << 24);
-            }
-            *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(s_tab) + 16u * u) = w;
-        }
-        __syncthreads();
-#pragma unroll
-        for (uint32_t q = 0; q < kPerL; ++q) {
-            const uint32_t i = (uint32_t)tid + q * kThreads;
-            if (i < ns) s_tab[e[q].x] = (uint16_t)e[q].y;
-        }
-    } else {
+    {
         const uint4* src = reinterpret_cast<const uint4*>(p.dense);
         uint4* dst = reinterpret_cast<uint4*>(s_tab);
         // LDS-DMA, every load in flight at once (one wave-instruction fills 1 KiB of LDS).  (A

@@ -1275,39 +1275,3 @@ def test_sparse_passes(case):
         assert runs[1] & 0xFFFF > 0, runs                             # taken
     elif case != "random_cyclic":
         assert runs[1] >> 16 == 1 and runs[1] & 0xFFFF > 0, runs      # reached the fixpoint
-
-
-@pytest.mark.parametrize("kind", ["top256", "mode1_byte_values", "mode2_self_valued", "no_byte_pairs",
-                                  "at_limit", "over_limit"])
-def test_byte_pass_table_written_or_copied(kind):
-    """Round 6: a map with at most 4096 byte-pair merge entries has its byte-pass table written in
-    LDS by the kernel (self tokens, then the merge entries), a larger one copied; both against the
-    oracle and against the copy forced (blt_debug_set_self_copy), on text and on random bytes with
-    odd chunk sizes."""
-    L = blt_amd._lib.lib()
-    rng = np.random.default_rng(abs(hash(kind)) % (1 << 31))
-    text = synth.text((1 << 20) + 333, seed=77)
-    if kind == "top256":
-        m = synth.merges_dict(synth.top_pair_merges(text, 256))
-    elif kind == "mode1_byte_values":        # merge values below 256: "merge" = the entry is not a
-        m = {(int(a), int(b)): int(v) for a, b, v in rng.integers(32, 127, (300, 3))}
-    elif kind == "mode2_self_valued":        # a merge valued its own first byte: marked entries
-        m = {(101, 32): 101, (116, 104): 116, (105, 110): 256}
-    elif kind == "no_byte_pairs":            # token keys only: the byte pass merges nothing
-        m = {(256, 257): 300, (300, 97): 301}
-    else:                                    # 4096 / 4097 byte-pair merges
-        k = 4096 if kind == "at_limit" else 4097
-        pairs = rng.choice(65536, k, replace=False)
-        m = {(int(p) >> 8, int(p) & 255): 256 + i for i, p in enumerate(pairs)}
-    s = blt_amd.BpeStrategy(m)
-    data = np.concatenate([text, rng.integers(0, 256, 300_001, dtype=np.uint8)])
-    for cs in (65537, 1 << 20):
-        exp = O.COracle(m).run(data, cs, threads=8)
-        got = s.process_chunks(data, cs)
-        prev = L.blt_debug_set_self_copy(1)
-        try:
-            got_copy = s.process_chunks(data, cs)
-        finally:
-            L.blt_debug_set_self_copy(prev)
-        assert np.array_equal(got, exp), (kind, cs)
-        assert np.array_equal(got_copy, exp), (kind, cs)

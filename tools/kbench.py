@@ -24,16 +24,10 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("BLT_LIB_PATH", "product")))
-    ap.add_argument("--self-copy", action="store_true", help="copy the byte pass's table even for small maps")
-    ap.add_argument("--ab-self-copy", action="store_true",
-                    help="alternate the table copy hook per launch: two medians from one process")
     a = ap.parse_args()
     import torch
     import blt_amd
     from blt_amd import synth
-    if a.self_copy:
-        blt_amd._lib.lib().blt_debug_set_self_copy(1)
-        a.tag += "+selfcopy"
 
     n = a.mib << 20
     m3 = synth.merges_dict(synth.text_merges_50k(synth.text(64 << 20, seed=3), seed=3))
@@ -64,17 +58,15 @@ def main():
         ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
         sp = torch.cuda.current_stream().cuda_stream
         tok = s.encode_device(d_in.data_ptr(), nb, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp, sync=True)
-        ts, tb = [], []
-        for rep in range(a.reps * (2 if a.ab_self_copy else 1)):
-            if a.ab_self_copy:
-                blt_amd._lib.lib().blt_debug_set_self_copy(rep & 1)
+        ts = []
+        for _ in range(a.reps):
             s.workspace_reset(ws.data_ptr(), nb, CHUNK, sp)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             s.encode_device_prezeroed(d_in.data_ptr(), nb, CHUNK, d_out.data_ptr(), ws.data_ptr(), wsb, sp)
             e1.record()
             torch.cuda.synchronize()
-            (tb if a.ab_self_copy and rep & 1 else ts).append(e0.elapsed_time(e1))
+            ts.append(e0.elapsed_time(e1))
         err = None
         try:
             s.check_workspace(ws.data_ptr(), sp)
@@ -83,9 +75,6 @@ def main():
         ms = float(np.median(ts))
         r = {"tag": a.tag, "cfg": cfg, "ms": round(ms, 4), "min_ms": round(min(ts), 4),
              "frac": round((nb + 2 * tok) / ms / 1e6 / 8000.0, 4), "tokens_per_byte": round(tok / nb, 4)}
-        if tb:
-            r["copy_ms"] = round(float(np.median(tb)), 4)
-            r["copy_min_ms"] = round(min(tb), 4)
         if err:
             r["err"] = err
         if a.check:
