@@ -907,21 +907,11 @@ struct SparseHostLease {
 // counters and the chain block.  Passes went on past four: more batches, one read each, then the
 // compaction (the caller reads the totals).  Nothing changes when the gate word (done and fallback
 // words) is set or detect's seeds overflow the lists (not taken).
-// One sparse batch at a time per device.  sparse_list_kernel and sparse_move_kernel wait for
-// lower-numbered workgroups (workgroups run in blockIdx order on each XCD, which makes that safe for
-// one such kernel on the device); two of them on different streams could each fill an XCD with
-// waiters whose predecessors sit behind the other's (the dispatch order interleaves XCDs, so a
-// later workgroup of one kernel can be resident while an earlier one waits for an XCD the other
-// kernel holds).  A batch takes the device's lock, waits (on the host) for the previous
-// batch's kernels when they ran on another stream, enqueues its own and records an event after
-// them: no two batches' kernels overlap, and a lone caller (one stream) never waits.
-struct SparseDevLock {
-    std::mutex mu;
-    hipEvent_t last = nullptr;        // after the last batch's kernels
-    hipStream_t last_stream = nullptr;
-};
-SparseDevLock g_sparse_dev[kMaxDevices];
-
+// Concurrent runs (threads sharing a handle, several handles, several processes on one device)
+// need no coordination: the two kernels whose workgroups wait for other workgroups
+// (sparse_list_kernel, sparse_move_kernel) take their work from tickets, so a workgroup only waits
+// for lower tickets, held by workgroups that have started (round 5 serialised the batches per
+// device with a lock and an event, because those kernels relied on blockIdx dispatch order).
 int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
                uint8_t* d_out, const uint64_t* n_dev, uint64_t n_max, const uint64_t* gate, uint64_t k,
                const uint64_t* off_in, uint64_t* off_out, uint64_t* tot, SparseRun* r) {
@@ -930,18 +920,6 @@ int run_sparse(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uin
     SparseHost* hb = lease.p;
     if (!L.sp_cap || !hb || n_max == 0 || n_max >= (1ull << 32)) return 0;
     if (dev < 0 || dev >= kMaxDevices) return fail(BLT_E_NODEV, "device index %d out of range", dev);
-    SparseDevLock& dl = g_sparse_dev[dev];
-    std::lock_guard<std::mutex> lk(dl.mu);
-    if (dl.last && dl.last_stream != s) HIP_TRY(hipEventSynchronize(dl.last));
-    if (!dl.last) HIP_TRY(hipEventCreateWithFlags(&dl.last, hipEventDisableTiming));
-    struct Mark {   // the event after this batch's kernels (every return path, errors included)
-        SparseDevLock& dl;
-        hipStream_t s;
-        ~Mark() {
-            if (hipEventRecord(dl.last, s) == hipSuccess) dl.last_stream = s;
-            else (void)hipStreamSynchronize(s), dl.last_stream = s;
-        }
-    } mark{dl, s};
     uint32_t* ctr = reinterpret_cast<uint32_t*>(ws + L.sp_ctr);
     blt::SparseParams q{};
     q.tok = reinterpret_cast<uint16_t*>(d_out);

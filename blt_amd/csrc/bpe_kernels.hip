@@ -3291,7 +3291,7 @@ __global__ __launch_bounds__(1024) void sparse_sample_kernel(SparseParams q) {
 
 // Bitmap words per workgroup of sparse_list_kernel (whole rounds of 4096, at most kListBlocks
 // workgroups).
-constexpr uint32_t kListWords = 16 * 256, kListBlocks = 2048;
+constexpr uint32_t kListWords = 16 * 256, kListBlocks = 512;
 __host__ __device__ __forceinline__ uint64_t sp_list_words(uint64_t nwords) {   // bitmap words per workgroup
     const uint64_t r = (nwords + (uint64_t)kListBlocks * kListWords - 1) / ((uint64_t)kListBlocks * kListWords);
     return (r ? r : 1ull) * kListWords;
@@ -3406,8 +3406,8 @@ __global__ __launch_bounds__(256) void sparse_detect_kernel(SparseParams qa) {
 // loads): it counts its seeds, publishes the count in its status word, and sums the published
 // counts of the workgroups before it (at most kListBlocks - 1 words, read at once by its threads):
 // its place in the list.  Its seeds then go out in position order, one workgroup scan per round.
-// Workgroups run in blockIdx order on every XCD, so every count waited for is published by a
-// running or finished workgroup.  (A first pass that reads its bitmap directly, a lane per word,
+// Its block comes from a ticket, so every count waited for is published by a running or finished
+// workgroup.  (A first pass that reads its bitmap directly, a lane per word,
 // measured 549 us on selfval against 20 us from this list: a lane walks its word's seeds one after
 // another, and a long run's seeds sit in few words.  On selfval: rounds of 256 words and one atomic
 // per workgroup on the list's counter, 45 us; one round, 31 us (the atomics serialise, ~11 ns each
@@ -3419,15 +3419,24 @@ constexpr uint64_t kListPub = 1ull << 62;   // a list workgroup's count is publi
 __global__ __launch_bounds__(256) void sparse_list_kernel(SparseParams qa) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_pre[4];
-    __shared__ uint32_t s_bad;
+    __shared__ uint32_t s_bad, s_b;
     if (sp_gated(qa)) return;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // (the detect gate: not taken) read once for the workgroup: another workgroup of this kernel may
-    // set the flags meanwhile, and every wave must reach the barriers below
-    if (tid == 0) s_bad = *qa.flags & 2u;
+    // set the flags meanwhile, and every wave must reach the barriers below.  The workgroup's block
+    // of words from a ticket (round 6): the counts it waits for are those of lower tickets, whose
+    // workgroups have started and publish theirs before waiting for anything (no reliance on the
+    // order workgroups are dispatched in; at most kListBlocks atomics).
+    if (tid == 0) {
+        s_bad = *qa.flags & 2u;
+        s_b = s_bad ? 0u : atomicAdd(qa.super_cnt + 1, 1u);   // (zeroed with the run's counters)
+    }
     __syncthreads();
     if (s_bad) return;
-    const uint64_t nwords = (*qa.n_dev + 31) / 32, per = sp_list_words(nwords);
+    const uint32_t b = s_b;
+    // words per workgroup from the host's bound qa.n, as the launcher sized the grid with (from the
+    // device's count, which may cross a round boundary the bound does not, the grid could fall short)
+    const uint64_t nwords = (*qa.n_dev + 31) / 32, per = sp_list_words((qa.n + 31) / 32);
     const uint64_t wb0 = (uint64_t)b * per, wb1 = wb0 + per < nwords ? wb0 + per : nwords;
     if (wb0 >= nwords) return;   // (uniform; no later workgroup has words either)
     auto load16 = [&](uint64_t w0, uint32_t (&m)[16]) {
@@ -3685,16 +3694,20 @@ __global__ __launch_bounds__(256) void sparse_apply_kernel(SparseParams q) {
 // Compaction of the hole layout in place.  The apply kernels counted the holes per tile of 8192
 // positions; one workgroup scans the counts (a tile's output position is its first position less the
 // holes before it; per-block sums over the counts cost more than that kernel).  A workgroup per
-// kMoveTiles consecutive tiles, in blockIdx order (8192 positions a tile: 8-token groups, four per
-// thread, consecutive lanes on consecutive groups), loads their input at once and marks it read, then
-// per tile stages its tokens in LDS, waits until every earlier tile whose input its output range
-// overlaps has marked its own (the output of tile T lies in [0, end of T's input): the one or two
-// tiles its range falls in), and writes the range with 16-byte stores (2-byte ones at the two partial
-// ends, which the neighbouring tiles share).  Small workgroups, many per CU (seven waves per SIMD):
-// the loads of the tiles in flight hide each other's latency.  Tiles in blockIdx order, not from a
-// ticket (one atomic per tile on one word: 399 us on selfval, ~11 ns per ticket): every XCD dispatches
-// its workgroups in order, so the lowest unfinished tile is running and waits for nobody, and a wait
-// on a lower tile always ends.
+// kMoveGroup consecutive tiles (8192 positions a tile: 8-token groups, four per thread, consecutive
+// lanes on consecutive groups), loads their input at once and marks it read, then per tile stages its
+// tokens in LDS, waits until every earlier tile whose input its output range overlaps has marked its
+// own (the output of tile T lies in [0, end of T's input): the one or two tiles its range falls in),
+// and writes the range with 16-byte stores (2-byte ones at the two partial ends, which the
+// neighbouring tiles share).  Small workgroup halves, many per CU (six waves per SIMD): the loads of
+// the tiles in flight hide each other's latency.
+// Progress (round 6): a workgroup's tiles come from a ticket (one atomic per
+// workgroup), so every tile a workgroup waits for belongs to a lower ticket, i.e. to a workgroup
+// that has started, loaded its tiles and marked them before any wait of its own; the lowest
+// unfinished ticket waits for nobody.  No assumption on the order the hardware dispatches
+// workgroups in, and none on other kernels sharing the device (round 5 relied on blockIdx order per
+// XCD, and two such kernels on two streams could starve each other).  Four tiles per ticket keep the
+// atomics (~11 ns each on one word, tools/atomic_probe.hip) at a quarter of round 4's one per tile.
 constexpr int kCpThreads = 256;
 constexpr uint64_t kMvRead = 1ull << 61;   // a tile's input is read (the list kernel's published counts use bit 62)
 static_assert(kSparseTile == 32u * kCpThreads, "compaction tile");
@@ -3760,20 +3773,31 @@ __global__ __launch_bounds__(1024) void sparse_tile_scan_kernel(SparseParams qa,
     if (tid == 0) *q.super_cnt = s_carry;
 }
 
-// Two consecutive tiles per workgroup, both loaded at once (twice the loads in flight per
-// workgroup at 7 waves per SIMD: selfval 0.699-0.710 -> 0.694 ms; four tiles spill)
-constexpr int kMoveTiles = 2;
-__global__ __launch_bounds__(kCpThreads) __attribute__((amdgpu_waves_per_eu(kMoveTiles == 1 ? 8 : 6)))
+// A workgroup is two halves of kCpThreads threads; each half takes two consecutive tiles and loads
+// both at once (twice the loads in flight per half at 6 waves per SIMD: selfval 0.699-0.710 ->
+// 0.694 ms in round 5; four tiles per half spill).  The halves run the same steps between the
+// workgroup's barriers; a half without a tile (the grid's last workgroup) only keeps step.
+constexpr int kMoveTiles = 2;                    // tiles per half
+// (Measured on selfval, round 6: one half per workgroup, 2 tiles per ticket, 0.737-0.754 ms; two,
+// 0.715-0.722; three, 0.720-0.724.)
+constexpr int kMoveHalves = 2;
+constexpr int kMoveGroup = kMoveTiles * kMoveHalves;   // tiles per ticket
+__global__ __launch_bounds__(kCpThreads * kMoveHalves) __attribute__((amdgpu_waves_per_eu(6)))
 void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
     // staged tokens, shifted by the output's offset in its 8-token group so that every output group
     // is one aligned 16-byte LDS word
-    __shared__ __attribute__((aligned(16))) uint16_t s_out[kSparseTile + 8];
-    __shared__ uint32_t s_wsum[4][kCpThreads / 64];
+    __shared__ __attribute__((aligned(16))) uint16_t s_out[kMoveHalves][kSparseTile + 8];
+    __shared__ uint32_t s_wsum[kMoveHalves][4][kCpThreads / 64];
+    __shared__ uint32_t s_tk, s_bad[kMoveHalves];
     if (sp_compact_skip(qa, nseeds0)) return;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int half = (int)threadIdx.x / kCpThreads;
+    const int tid = (int)threadIdx.x % kCpThreads, lane = tid & 63, wave = tid >> 6;
     const uint64_t n = *qa.n_dev, ntiles = (n + kSparseTile - 1) / kSparseTile;
-    const uint64_t T0 = (uint64_t)blockIdx.x * kMoveTiles;
-    if (T0 >= ntiles) return;   // (uniform: the grid is sized for the host's count, >= the device's)
+    if (threadIdx.x == 0) s_tk = atomicAdd(qa.super_cnt + 2, 1u);   // (zeroed with the run's counters)
+    __syncthreads();
+    const uint64_t G0 = (uint64_t)s_tk * kMoveGroup;
+    if (G0 >= ntiles) return;   // (uniform: the grid is sized for the host's count, >= the device's)
+    const uint64_t T0 = G0 + (uint64_t)half * kMoveTiles;
     // level j of tile t: 8-token group G = j * kCpThreads + tid
     uint32_t w[kMoveTiles][4][4], valid[kMoveTiles][4];
 #pragma unroll
@@ -3799,21 +3823,19 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
             }
         }
     }
-    if (kMoveTiles > 1) {
-        // every tile of the workgroup marked read at once: a mark published only when the tile's
-        // turn comes chains the workgroups (the first tile of workgroup b waits for the last one
-        // of workgroup b - 1, which waits for its first ...: measured 30.8 ms on selfval)
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): every load of the workgroup's tiles
-        __syncthreads();
-        if (tid < kMoveTiles && T0 + tid < ntiles) st_publish(qa.status + T0 + tid, kMvRead);
-    }
+    // every tile of the workgroup marked read at once: a mark published only when the tile's turn
+    // comes chains the workgroups (the first tile of workgroup b waits for the last one of
+    // workgroup b - 1, which waits for its first ...: measured 30.8 ms on selfval)
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): every load of the workgroup's tiles
+    __syncthreads();
+    if (threadIdx.x < (uint32_t)kMoveGroup && G0 + threadIdx.x < ntiles) st_publish(qa.status + G0 + threadIdx.x, kMvRead);
 #pragma unroll
     for (int t = 0; t < kMoveTiles; ++t) {
         const uint64_t T = T0 + t;
-        if (T >= ntiles) break;   // (uniform)
+        const bool here = T < ntiles;   // (uniform per half; the halves keep step at every barrier)
         const uint64_t tile0 = T * kSparseTile;
-        const uint32_t hb = qa.tile_cnt[T];   // holes before the tile (sparse_tile_scan_kernel)
-        const uint32_t hnext = T + 1 < ntiles ? qa.tile_cnt[T + 1] : *qa.super_cnt;
+        const uint32_t hb = here ? qa.tile_cnt[T] : 0u;   // holes before the tile (sparse_tile_scan_kernel)
+        const uint32_t hnext = !here ? 0u : T + 1 < ntiles ? qa.tile_cnt[T + 1] : *qa.super_cnt;
         const uint64_t O = tile0 - hb;
         const uint32_t e = (uint32_t)(O & 7u);
         uint32_t cnt[4], incl[4];
@@ -3822,7 +3844,7 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
         for (int j = 0; j < 4; ++j) {
             cnt[j] = __popc(valid[t][j]);
             incl[j] = wave_incl_scan(cnt[j], lane);
-            if (lane == 63) s_wsum[j][wave] = incl[j];
+            if (lane == 63) s_wsum[half][j][wave] = incl[j];
         }
         __syncthreads();
         uint32_t lbase = e;
@@ -3831,36 +3853,33 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
             uint32_t wb = 0, lt = 0;
 #pragma unroll
             for (int k = 0; k < kCpThreads / 64; ++k) {
-                const uint32_t v = s_wsum[j][k];
+                const uint32_t v = s_wsum[half][j][k];
                 wb += k < wave ? v : 0u;
                 lt += v;
             }
             uint32_t o = lbase + wb + incl[j] - cnt[j];
             if (valid[t][j] == 0xFFu && (o & 1u) == 0u) {
-                uint32_t* d = reinterpret_cast<uint32_t*>(s_out) + (o >> 1);
+                uint32_t* d = reinterpret_cast<uint32_t*>(s_out[half]) + (o >> 1);
                 d[0] = w[t][j][0]; d[1] = w[t][j][1]; d[2] = w[t][j][2]; d[3] = w[t][j][3];
             } else {
 #pragma unroll
                 for (uint32_t k = 0; k < 8; ++k) {
-                    if ((valid[t][j] >> k) & 1u) s_out[o++] = (uint16_t)(w[t][j][k >> 1] >> (16u * (k & 1u)));
+                    if ((valid[t][j] >> k) & 1u) s_out[half][o++] = (uint16_t)(w[t][j][k >> 1] >> (16u * (k & 1u)));
                 }
             }
             lbase += lt;
         }
         const uint32_t ttot = lbase - e + ((qa.inject & kInjectSparseMove) ? 1u : 0u);   // (test hook)
         const uint64_t in_end = tile0 + kSparseTile < n ? tile0 + kSparseTile : n;
-        __syncthreads();   // staged: every load of the tile done
         // the tile's count against the scan's hole counts (the bitmap against the apply kernels'
         // counters): a tile whose counts disagree, or whose output would not lie within its own
         // input, flags error bit 4 and writes nothing
-        const bool counts_ok = ttot == (in_end - tile0) - (hnext - hb) && hb <= tile0 && O + ttot <= in_end;
-        if (tid == 0) {
-            if (kMoveTiles == 1) st_publish(qa.status + T, kMvRead);
-            if (!counts_ok) flag_error(qa.ctl, qa.sticky, 4u);
-        }
+        const bool counts_ok = here && ttot == (in_end - tile0) - (hnext - hb) && hb <= tile0 && O + ttot <= in_end;
+        if (tid == 0 && here && !counts_ok) flag_error(qa.ctl, qa.sticky, 4u);
         const bool moves = counts_ok && !(O == tile0 && ttot == in_end - tile0);   // (else in place already)
-        if (!moves) continue;   // (uniform)
-        if (wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
+        if (tid == 0) s_bad[half] = 0u;
+        __syncthreads();   // staged: every load of the tile done
+        if (moves && wave == 0) {   // the earlier tiles whose input the output range overlaps (one or two)
             bool bad = false;
             const uint64_t ulast = ttot ? (O + ttot - 1) / kSparseTile : 0;
             const uint64_t uend = ulast + 1 < T ? ulast + 1 : T;
@@ -3873,12 +3892,12 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
             }
             if (__ballot(bad) != 0ull && lane == 0) {
                 flag_error(qa.ctl, qa.sticky, 1u);
-                s_wsum[0][0] = ~0u;   // (after the barrier below: every wave has read s_wsum)
+                s_bad[half] = 1u;
             }
         }
         __syncthreads();
         // a wait that timed out (flagged): the input it waited for may be unread, so nothing is written
-        if (s_wsum[0][0] == ~0u) continue;   // (uniform)
+        if (!moves || s_bad[half]) continue;   // (uniform per half; no barrier before the next tile's)
         // output groups r = 0 .. nr - 1 (global tokens 8 (O / 8 + r) ..): whole ones with one 16-byte
         // store, the partial first and last token by token
         const uint32_t nr = (e + ttot + 7u) / 8u;
@@ -3886,11 +3905,11 @@ void sparse_move_kernel(SparseParams qa, const uint32_t* nseeds0) {
         for (uint32_t r = (uint32_t)tid; r < nr; r += kCpThreads) {
             const uint32_t b = 8u * r;
             if (b >= e && b + 8u <= e + ttot) {
-                const v4u v = *reinterpret_cast<const v4u*>(s_out + b);
+                const v4u v = *reinterpret_cast<const v4u*>(s_out[half] + b);
                 __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(dst + b));
             } else {
                 for (uint32_t k = b; k < b + 8u; ++k)
-                    if (k >= e && k < e + ttot) dst[k] = s_out[k];
+                    if (k >= e && k < e + ttot) dst[k] = s_out[half][k];
             }
         }
     }
@@ -3966,8 +3985,8 @@ hipError_t launch_sparse_compact(const SparseParams& q, const uint32_t* nseeds0,
     if (!sparse_ok(q) || !q.total || !nseeds0 || !q.nchunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (q.n + kSparseTile - 1) / kSparseTile;
     hipLaunchKernelGGL(sparse_tile_scan_kernel, dim3(1), dim3(1024), 0, s, q, nseeds0);
-    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)((ntiles + kMoveTiles - 1) / kMoveTiles)), dim3(kCpThreads), 0, s,
-                       q, nseeds0);
+    hipLaunchKernelGGL(sparse_move_kernel, dim3((unsigned)((ntiles + kMoveGroup - 1) / kMoveGroup)),
+                       dim3(kCpThreads * kMoveHalves), 0, s, q, nseeds0);
     hipLaunchKernelGGL(sparse_coff_kernel, dim3((unsigned)q.nchunks), dim3(64), 0, s, q, nseeds0);
     return hipGetLastError();
 }

@@ -1275,3 +1275,36 @@ def test_sparse_passes(case):
         assert runs[1] & 0xFFFF > 0, runs                             # taken
     elif case != "random_cyclic":
         assert runs[1] >> 16 == 1 and runs[1] & 0xFFFF > 0, runs      # reached the fixpoint
+
+
+def test_sparse_list_rounds_across_the_bound():
+    """Round 6: the seed list's words per workgroup come from the host's bound on the token count (the
+    input's bytes), not from the count on the device.  An input just past 512 x 4096 bitmap words
+    (2^26 positions) whose byte pass leaves fewer tokens than that: sized from the device's count,
+    each workgroup took half the words the launcher had planned, and the grid fell short of the
+    list's end (seeds lost, merges missed)."""
+    import torch
+    m, cs = synth.SELF_VALUED_MAP, 16 << 20
+    data = synth.text((64 << 20) + (1 << 20) + 13, seed=31)
+    exp, elens = O.COracle(m).run(data, cs, threads=16, return_lens=True)
+    s = blt_amd.BpeStrategy(m)
+    n = data.size
+    nch = (n + cs - 1) // cs
+    d_in = torch.from_numpy(data).cuda()
+    d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+    d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+    wsb = s.workspace_size(n, cs)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    prev = _sparse(1)
+    try:
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream, d_off.data_ptr(),
+                              sync=True)
+        torch.cuda.synchronize()
+        sp = int(blt_amd._lib.lib().blt_debug_last_sparse())
+    finally:
+        _sparse(prev)
+    assert sp & 0xFFFF, hex(sp)
+    assert tok * 2 == exp.size
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    assert np.array_equal(np.diff(d_off.cpu().numpy()) * 2, elens)
