@@ -14,7 +14,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 # the stamps exist only in the timing build of the kernel (make exp; -DBLT_TIMING)
-os.environ.setdefault("BLT_LIB_PATH", os.path.join(ROOT, "build", "exp", "libblt_bpe_timing.so"))
+os.environ.setdefault("BLT_LIB_PATH", os.path.join(ROOT, "build", "xp", "libblt_bpe_timing.so"))
 import torch  # noqa: E402
 
 import blt_amd  # noqa: E402
