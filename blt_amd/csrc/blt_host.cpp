@@ -607,7 +607,7 @@ inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
-    uint64_t ctl, status, total, off_a, off_b, cmap, gstat, bytes, zero_bytes;
+    uint64_t ctl, status, status2, total, off_a, off_b, cmap, cmap_stride, gstat, bytes, zero_bytes;
     // sparse passes of a cyclic map (run_sparse): bitmaps of n bits, seed and merge lists of
     // sp_cap entries, compaction tile words, counters; sp_cap 0 when the map cannot use them
     uint64_t sp_holes, sp_bits0, sp_bits1, sp_bits2, sp_seeds0, sp_seeds1, sp_merges, sp_tileo, sp_status, sp_ctr, sp_ntiles,
@@ -645,8 +645,12 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
     L.off_a = L.total + kChainBlock;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
     L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
-    L.gstat = L.cmap + up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));   // finish: a status word per group
-    L.bytes = single_pass ? L.cmap : L.gstat + up16(8 * L.nchunks);
+    // three chunk maps: u16 scan pass k reads map k % 3, builds k + 1's and zeroes k + 2's
+    L.cmap_stride = up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
+    L.gstat = L.cmap + 3 * L.cmap_stride;   // finish: a status word per group
+    // odd chained u16 scan passes' status words (even ones use pass 1's)
+    L.status2 = L.gstat + up16(8 * L.nchunks);
+    L.bytes = single_pass ? L.cmap : L.status2 + up16(8 * L.ntiles);
     if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
         const uint64_t bm = up16(4 * ((n + 31) / 32));
         const uint64_t cap = n / 16 + 4096;
@@ -704,11 +708,13 @@ struct Chain {
     uint32_t pass_id = 0;             // 1, 2, ...
 };
 
-// tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).
+// tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).  *map_ready (u16
+// passes of a chain): the previous pass was a scan pass, which built this pass's chunk map and reset
+// the status words; set for the next pass to whether this one was.
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
              uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr,
-             bool tok_scan = false) {
+             bool tok_scan = false, bool* map_ready = nullptr) {
     const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->byte_mode >= 0 && be;   // byte-pass fast kernel
     const uint64_t tile = columnar ? blt::kTilePosBytes
                                    : in_u16 ? (tok_scan ? blt::kTilePosTok : blt::kTilePosU16) : blt::kTilePos;
@@ -752,10 +758,27 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.debug = g_debug_tiles;
     p.inject = g_inject.load(std::memory_order_relaxed);
     p.sticky = h->sticky.load(std::memory_order_acquire);
-    p.cmap = reinterpret_cast<uint64_t*>(ws + L.cmap);
+    const bool scan16 = in_u16 && tok_scan;
+    const bool ready = scan16 && chain && map_ready && *map_ready;
+    if (scan16) {
+        const uint32_t r = chain ? chain->pass_id % 3u : 0u;
+        auto map = [&](uint32_t i) { return reinterpret_cast<uint64_t*>(ws + L.cmap + (uint64_t)(i % 3u) * L.cmap_stride); };
+        p.cmap = map(r);
+        if (chain && map_ready) {
+            // chained scan passes alternate status words and ticket words by pass parity; each
+            // zeroes the next pass's
+            const bool odd = chain->pass_id & 1u;
+            p.cmap_next = map(r + 1u);
+            p.cmap_zero = map(r + 2u);
+            p.status = reinterpret_cast<uint64_t*>(ws + (odd ? L.status2 : L.status));
+            p.status_zero = reinterpret_cast<uint64_t*>(ws + (odd ? L.status : L.status2));
+            p.tick = odd ? blt::kCtlTickAlt : 0u;
+        }
+    }
+    if (map_ready) *map_ready = scan16 && chain;
     p.ws_check = (ws_zeroed && !in_u16 && !chain) ? 1u : 0u;   // the caller's BLT_ENCODE_WORKSPACE_ZEROED
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, h->byte_mode, (chain && h->live_first) ? 1 : 0, dev, s));
-    else if (in_u16 && tok_scan) HIP_TRY(blt::launch_scan_tokens(p, dev, s));
+    else if (scan16) HIP_TRY(blt::launch_scan_tokens(p, ready ? 1 : 0, dev, s));
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }
@@ -1146,6 +1169,8 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     };
     t_last_fused = fused ? 1 : 0;
     uint64_t rec[4] = {0, 0, 0, 0};
+    // the previous launch was a u16 scan pass: the next scan pass's chunk map is built (run_pass)
+    bool map_ready = false;
     // the finish kernels, once per encode: at the first u16 pass whose input chunks may fit in LDS
     bool fin_tried = !g_finish.load(std::memory_order_relaxed);
     auto finish_now = [&](uint64_t kk) {
@@ -1164,6 +1189,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
+                map_ready = false;
                 if (out_tokens) {
                     // a caller that waits anyway: see whether the finish ran (its gate word, the longest
                     // chunk, fit in LDS) before enqueueing the passes it turned into no-ops
@@ -1175,7 +1201,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             }
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
-                                  false, &c, scan))
+                                  false, &c, scan, &map_ready))
                 return rc;
             cur ^= 1;
         }
@@ -1231,6 +1257,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), n, gate, k, off[cur], off[cur ^ 1],
                                 tot, &r))
             return rc;
+        map_ready = false;
         if (r.taken) {
             bool fin = false;
             if (int rc = sparse_taken(r, &fin)) return rc;
@@ -1240,12 +1267,14 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
             const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
-            if (finish_now(k))
+            if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
+                map_ready = false;
+            }
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
-                                  false, &c, scan))
+                                  false, &c, scan, &map_ready))
                 return rc;
             cur ^= 1;
         }
@@ -1265,6 +1294,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), N, nullptr, k, off[cur],
                                     off[cur ^ 1], tot, &r))
                 return rc;
+            map_ready = false;
             if (r.taken) {
                 bool fin = false;
                 if (int rc = sparse_taken(r, &fin)) return rc;

@@ -16,6 +16,7 @@ constexpr uint64_t kTilePosBytes = 32768;      // positions per look-back tile o
 constexpr uint64_t kMinChunkBytes = 4096;      // byte pass needs chunk_size >= positions per wave range
 constexpr uint64_t kCtlBytes = 64;            // control block ahead of the status words
 constexpr uint32_t kCtlLeft = 15;             // ctl word: workgroups of a single-pass launch that have left
+constexpr uint32_t kCtlTickAlt = 12;          // ctl word: the ticket of odd chained u16 scan passes
 constexpr uint32_t kCtlCover = 14;            // ctl word: status words [0, ctl[14]) are known zero (set by
                                               // blt_bpe_workspace_reset and by a single-pass launch's self-reset);
                                               // a launch told its workspace is zeroed checks its tiles against it
@@ -54,6 +55,12 @@ struct PassParams {
                                // component); later passes return at once
     uint32_t pass_id;          // u16 passes: 1, 2, ... (pass k writes totals and chunk offsets [k & 1])
     uint64_t* cmap;            // u16 scan kernel: chunk-map word per wave range of kTokRange tokens
+    uint64_t* cmap_next;       // u16 scan kernel (nullable): the next pass's chunk map, built from this
+                               // pass's chunk offsets as it writes them (zeroed before this pass)
+    uint64_t* cmap_zero;       // u16 scan kernel (nullable): the map the pass after next builds, zeroed here
+    uint64_t* status_zero;     // u16 scan kernel (nullable): the next pass's status words (the other of two
+                               // arrays), zeroed here with its ticket word ctl[tick ^ kCtlTickAlt]
+    uint32_t tick;             // ctl word of the tile tickets: 0, or kCtlTickAlt for odd chained u16 passes
     uint64_t cs_magic;         // cs > 0: floor((2^64 - 1) / cs), for x / cs by a high multiply
     uint32_t cs_tiles;         // cs / kTilePosBytes when cs is a whole number of byte-pass tiles
                                // (below 2^31), else 0
@@ -92,9 +99,10 @@ hipError_t launch_scan_bytes(const PassParams& p, int mode, int live, int device
 // done word value of a byte pass after which nothing merges (u16 pass k writes k)
 constexpr uint32_t kDoneBytePass = 0x80000000u;
 // u16 pass of a general map on the scan kernel (seg::scan_tokens_kernel), in place (p.in may equal
-// p.out): chunk map of p.cstart into p.cmap, then the scan.  Needs every chunk but the last to hold
-// at least kTokRange tokens.
-hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s);
+// p.out): when map_ready is 0, the chunk map of p.cstart into p.cmap first (and the status words and
+// ticket zeroed); with map_ready the previous scan pass built p.cmap and reset its status words and
+// ticket itself.  Needs every chunk but the last to hold at least kTokRange tokens.
+hipError_t launch_scan_tokens(const PassParams& p, int map_ready, int device, hipStream_t s);
 // Passes 1 and 2 of a general map in one kernel (seg::scan_tokens_kernel<kHash, true>): bytes in,
 // the second pass's big-endian tokens out, for maps whose bucket table fits in LDS and chunk sizes
 // >= kMinChunkBytes.  A wave range takes the first pass's carry-in from the 64 bytes before it

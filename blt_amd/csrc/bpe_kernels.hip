@@ -1921,6 +1921,17 @@ static_assert(kGroupsTok <= 64 && kS * kWaves <= 64, "groups");
 // one; bits 32..63 the start's chunk index.
 constexpr uint32_t kCmStart = 1u << 11, kCmEnd = 1u << 23;
 
+// The next pass's chunk-map words for chunk c starting at output token P (round 6): the start in
+// P's wave range, the end of chunk c - 1 in the range of P - 1.  The two marks of one word can come
+// from two tiles on two XCDs: agent-scope ORs into a map zeroed one pass earlier.  (It replaces a
+// chunk_map_kernel launch per u16 pass, 4.8 us plus its launch gap on the chain row.)
+__device__ __forceinline__ void cm_mark(uint64_t* m, uint64_t P, uint32_t c) {
+    __hip_atomic_fetch_or(m + (P >> 10), (P & 1023u) | kCmStart | ((uint64_t)c << 32), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    if (c) __hip_atomic_fetch_or(m + ((P - 1) >> 10), (((P - 1) & 1023u) << 12) | kCmEnd, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint64_t token_count(const PassParams& p) {
     return p.n_dev ? __hip_atomic_load(const_cast<uint64_t*>(p.n_dev), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p.n;
 }
@@ -1964,7 +1975,8 @@ __global__ __launch_bounds__(256) void chunk_map_kernel(PassParams p) {
     if (done) return;
     const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (r < (n + kTileTok - 1) / kTileTok) p.status[r] = 0ull;
-    if (r == 0) { p.ctl[0] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
+    if (p.cmap_next && r < (n + kWavePos - 1) / kWavePos) p.cmap_next[r] = 0ull;   // the scan ORs into it
+    if (r == 0) { p.ctl[p.tick] = 0u; p.ctl[kCtlCover] = 0u; }   // this pass dirties the status words
     const uint64_t nc = p.nchunks;
     const bool in_lds = nc <= kCmLds;
     if ((uint64_t)blockIdx.x * 256u * kWavePos >= n) return;   // uniform: no range of this block is live
@@ -2135,7 +2147,10 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const bool cstart = has_coff && (cwl & kCmStart) != 0u;
     if (__ballot(st.mv[j] != 0xFFFFFFFFu) == 0) {
         // dense: every pair merges, so the only possible chunk start is the range's first token
-        if (cstart && lane == 0) KARG(chunk_off)[cwh] = O + goff;
+        if (cstart && lane == 0) {
+            KARG(chunk_off)[cwh] = O + goff;
+            if (inplace && p.cmap_next) cm_mark(p.cmap_next, O + goff, cwh);
+        }
         emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
     }
@@ -2149,8 +2164,11 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
     const uint32_t L = ~((M << 1) | (c ^ 1u)) & vmask;
     if (cstart) {
         const uint32_t e = (cwl & 0x7FFu) - lane16_here();
-        if (e < 16u)
-            KARG(chunk_off)[cwh] = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+        if (e < 16u) {
+            const uint64_t P = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
+            KARG(chunk_off)[cwh] = P;
+            if (inplace && p.cmap_next) cm_mark(p.cmap_next, P, cwh);
+        }
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
     // in place: output = input when nothing merged before this range or in it
@@ -2443,9 +2461,27 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                     (__attribute__((address_space(3))) void*)(dst + u0), 16, 0, 0);
         }
     }
+    if constexpr (!kFused) {
+        // Chained u16 passes (round 6): the next pass's status words and ticket word (the other of
+        // two sets; the previous pass used them) and the map the pass after next builds (the one the
+        // previous pass read) are zeroed here over the live workgroups; this pass's own were zeroed by
+        // the previous pass, or by chunk_map_kernel before the first.  No count-out at the end: the
+        // next pass needs nothing from this one's tail.
+        const uint64_t live = gridDim.x < ntiles ? gridDim.x : ntiles;
+        if (p.cmap_zero) {
+            const uint64_t nr = (n + kWavePos - 1) / kWavePos;
+            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < nr; i += live * kThreads) p.cmap_zero[i] = 0ull;
+        }
+        if (p.status_zero)
+            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < ntiles; i += live * kThreads) p.status_zero[i] = 0ull;
+        if (blockIdx.x == 0 && tid == 0) {
+            if (p.status_zero) p.ctl[p.tick ^ kCtlTickAlt] = 0u;
+            p.ctl[kCtlCover] = 0u;   // this pass dirties the status words
+        }
+    }
     if (tid == 0) {
-        s_tk[kRing - 2] = atomicAdd(p.ctl, 1u);   // T
-        s_tk[kRing - 1] = atomicAdd(p.ctl, 1u);   // Tq, the tile after it
+        s_tk[kRing - 2] = atomicAdd(p.ctl + p.tick, 1u);   // T
+        s_tk[kRing - 1] = atomicAdd(p.ctl + p.tick, 1u);   // Tq, the tile after it
         for (int r = 0; r < kRing; ++r) s_p1cnt[r] = 0;
         s_rdone = 0; s_lbdone = 0; s_tkdone = 0;
     }
@@ -2494,7 +2530,7 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
                 else load_tok(p, n, Tq, wave, lane, xq, nxtq, cwq);
             }
             uint32_t tk = kNone;
-            if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl, 1u);
+            if (tid == kTkTid && Tq < ntiles) tk = atomicAdd(p.ctl + KARG(tick), 1u);
             asm volatile("" ::: "memory");
 
             bool lbw = wave == 0;
@@ -3126,11 +3162,11 @@ hipError_t launch_scan_bytes(const PassParams& p, int mode, int live, int device
     return hipGetLastError();
 }
 
-hipError_t launch_scan_tokens(const PassParams& p, int device, hipStream_t s) {
+hipError_t launch_scan_tokens(const PassParams& p, int map_ready, int device, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
     // p.n bounds the token count the kernels read from p.n_dev
     const uint64_t ranges = (p.n + kTokRange - 1) / kTokRange;
-    hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
+    if (!map_ready) hipLaunchKernelGGL(seg::chunk_map_kernel, dim3((unsigned)((ranges + 255) / 256)), dim3(256), 0, s, p);
     const bool lds = p.hbytes <= kHashLdsMax;
     const int mode = lds ? (p.hone ? 2 : 1) : 0;
     const void* fn = mode == 2 ? (const void*)seg::scan_tokens_kernel<2>

@@ -81,7 +81,7 @@ for st in "$@"; do
     proff2)
       # proff2[:ROWS[:ENV]]  (ENV: NAME=VALUE for the profiled run)
       rows=${a:-multi,wrap,selfval,chain}
-      pd=prof_f2${a:+_${a//,/_}}${b:+_${b//=/}}
+      bt=${b##*/}; pd=prof_f2${a:+_${a//,/_}}${b:+_${bt//[=.]/_}}
       (cd /tmp && export TMPDIR=/tmp && { [ -z "$b" ] || export "$b"; } && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$O/$pd" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --only-configs "$rows" \
         > "$O/$pd.log" 2>&1)
