@@ -93,6 +93,9 @@ _DEBUG_SIGNATURES = {
     "blt_debug_set_tile_record": (None, [_vp]),
     "blt_debug_set_inject": (ctypes.c_uint32, [ctypes.c_uint32]),
     "blt_debug_last_u16_passes": (ctypes.c_uint32, []),
+    "blt_debug_last_scan_passes": (ctypes.c_uint32, []),
+    "blt_debug_set_u16_chain": (ctypes.c_int, [ctypes.c_int]),
+    "blt_debug_set_fused_only": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_set_shared_contexts": (None, [ctypes.c_int]),
     "blt_debug_set_pin_ring": (ctypes.c_int, [ctypes.c_int]),
     "blt_debug_set_fused": (None, [ctypes.c_int]),

@@ -594,16 +594,26 @@ std::atomic<int> g_shared_contexts{0};
 // Passes 1 and 2 of eligible general maps in one kernel (blt_debug_set_fused(0): the two-kernel
 // chain, for A/B runs and tests).
 std::atomic<int> g_fused{1};
+// Test hooks (blt_debug_set_u16_chain): bit 0 chained scan passes build the next pass's chunk map,
+// bit 1 the host extends the scan kernel's chunk bound from the offsets it reads.
+std::atomic<int> g_u16_chain{3};
+// Test hook (blt_debug_set_fused_only): a synchronous general-map encode that ran the fused kernel
+// returns right after it (its tokens in d_out, its count; chunk offsets not copied out).
+std::atomic<int> g_fused_only{0};
 constexpr uint32_t kEncodeNoFused = 1u << 31;   // internal encode_device flag: the two-kernel chain
 // Test hook: u16 passes the calling thread's last synchronous general-map encode ran before the
 // chain stopped (blt_debug_last_u16_passes).
 thread_local uint32_t t_last_u16_passes = 0;
+// Test hook: u16 passes the calling thread's last general-map encode enqueued on the scan kernel
+// (blt_debug_last_scan_passes).
+thread_local uint32_t t_last_scan_passes = 0;
 // Test hook: how the calling thread's last synchronous general-map encode ran passes 1 and 2:
 // 0 two kernels, 1 fused, 2 fused and fell back (blt_debug_last_fused).
 thread_local uint32_t t_last_fused = 0;
 
 // ---- workspace layout -------------------------------------------------------------------
 inline uint64_t up16(uint64_t x) { return (x + 15) & ~15ull; }
+inline uint64_t up256(uint64_t x) { return (x + 255) & ~255ull; }
 
 struct WsLayout {
     uint64_t ntiles, nchunks;
@@ -644,12 +654,13 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
                               // words: encode_device zeroes both at once)
     L.off_a = L.total + kChainBlock;
     L.off_b = L.off_a + up16(8 * (L.nchunks + 1));
-    L.cmap = L.off_b + up16(8 * (L.nchunks + 1));
-    // three chunk maps: u16 scan pass k reads map k % 3, builds k + 1's and zeroes k + 2's
-    L.cmap_stride = up16(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
+    // three chunk maps: u16 scan pass k reads map k % 3, builds k + 1's and zeroes k + 2's (each on
+    // cache lines of its own: one is zeroed while the next is marked)
+    L.cmap = up256(L.off_b + up16(8 * (L.nchunks + 1)));
+    L.cmap_stride = up256(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
     L.gstat = L.cmap + 3 * L.cmap_stride;   // finish: a status word per group
     // odd chained u16 scan passes' status words (even ones use pass 1's)
-    L.status2 = L.gstat + up16(8 * L.nchunks);
+    L.status2 = up256(L.gstat + up16(8 * L.nchunks));
     L.bytes = single_pass ? L.cmap : L.status2 + up16(8 * L.ntiles);
     if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
         const uint64_t bm = up16(4 * ((n + 31) / 32));
@@ -706,6 +717,7 @@ struct Chain {
     uint64_t* n_out = nullptr;        // this pass's count
     uint32_t* done = nullptr;         // set to its pass_id by the last pass that can merge anything
     uint32_t pass_id = 0;             // 1, 2, ...
+    bool next_scan = false;           // the next pass runs on the scan kernel too (it builds its chunk map)
 };
 
 // tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).  *map_ready (u16
@@ -759,6 +771,7 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.inject = g_inject.load(std::memory_order_relaxed);
     p.sticky = h->sticky.load(std::memory_order_acquire);
     const bool scan16 = in_u16 && tok_scan;
+    if (!(g_u16_chain.load(std::memory_order_relaxed) & 1)) map_ready = nullptr;
     const bool ready = scan16 && chain && map_ready && *map_ready;
     if (scan16) {
         const uint32_t r = chain ? chain->pass_id % 3u : 0u;
@@ -766,19 +779,24 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
         p.cmap = map(r);
         if (chain && map_ready) {
             // chained scan passes alternate status words and ticket words by pass parity; each
-            // zeroes the next pass's
+            // zeroes the next pass's (whatever kernel runs it: a chunk-map or merge pass zeroes its own)
             const bool odd = chain->pass_id & 1u;
-            p.cmap_next = map(r + 1u);
-            p.cmap_zero = map(r + 2u);
             p.status = reinterpret_cast<uint64_t*>(ws + (odd ? L.status2 : L.status));
             p.status_zero = reinterpret_cast<uint64_t*>(ws + (odd ? L.status : L.status2));
             p.tick = odd ? blt::kCtlTickAlt : 0u;
+            if (chain->next_scan) {   // the next pass's chunk map, built here
+                p.cmap_next = map(r + 1u);
+                p.cmap_zero = map(r + 2u);
+            }
         }
     }
-    if (map_ready) *map_ready = scan16 && chain;
+    if (map_ready) *map_ready = scan16 && chain && chain->next_scan;
     p.ws_check = (ws_zeroed && !in_u16 && !chain) ? 1u : 0u;   // the caller's BLT_ENCODE_WORKSPACE_ZEROED
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, h->byte_mode, (chain && h->live_first) ? 1 : 0, dev, s));
-    else if (scan16) HIP_TRY(blt::launch_scan_tokens(p, ready ? 1 : 0, dev, s));
+    else if (scan16) {
+        HIP_TRY(blt::launch_scan_tokens(p, ready ? 1 : 0, dev, s));
+        ++t_last_scan_passes;
+    }
     else HIP_TRY(blt::launch_merge_pass(p, in_u16 ? 1 : 0, be ? 1 : 0, dev, s));
     return 0;
 }
@@ -1123,6 +1141,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     // pass 1's control block and status words and the chain's totals are contiguous: one memset
     // (BLT_ENCODE_WORKSPACE_ZEROED is ignored here, as the header says)
     HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes + kChainBlock, s));
+    t_last_scan_passes = 0;
     const bool bounded = chain_bounded(h);
     // Passes 1 and 2 in one kernel (run_fused) when the bucket table fits in LDS, chunks hold whole
     // wave ranges, and the first pass need not end the chain itself (maps with byte-pair keys only
@@ -1142,6 +1161,10 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (int rc = run_fused(h, t, dev, s, ws, L, d_in, n, cs, d_out, off[1], tot + 1, done, fused_fail)) return rc;
         cur = 1;
         k = 2;
+        if (g_fused_only.load(std::memory_order_relaxed) && out_tokens) {
+            t_last_fused = 1;
+            return read_u64(tot + 1, out_tokens, s);
+        }
         if (bounded && h->chain_depth > 2) {
             // more passes to enqueue: see first whether the fused kernel resolved every range (a
             // failed one leaves them no-ops, but each costs its launch)
@@ -1185,7 +1208,8 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         // and chunk offsets.  Only a caller asking for the token count waits (once).
         const uint32_t k_last = h->chain_depth - 1;
         for (; k <= k_last; ++k) {
-            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
+            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k,
+                          k + 1 <= k_last && k + 1 < 64 && (cs >> (k + 1)) >= blt::kTokRange};
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
@@ -1264,25 +1288,53 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (fin) return 0;
         }
     }
+    // A lower bound of the chunks' token counts (the last chunk's aside) beyond cs >> k: min_in for
+    // the input of pass min_k, read from the chunk offsets at a batch end; a pass at most halves a
+    // chunk.  It keeps the scan kernel on chunks that stay long (cyclic_dense: one letter per word
+    // and pass, 16 MiB chunks of ~9 M tokens) past the pass where cs >> k falls below kTokRange, in
+    // place of merge_tokens_kernel at twice the time per pass.  (The scan still checks: two chunk
+    // starts or ends in one wave range flag error bit 16.)
+    uint64_t min_in = 0, min_k = 0;
+    std::vector<uint64_t> hoff;
+    const int u16c = g_u16_chain.load(std::memory_order_relaxed);
+    auto scan_ok = [&](uint64_t kk) {
+        if (kk >= 64) return false;
+        if ((cs >> kk) >= blt::kTokRange) return true;
+        if (!(u16c & 2)) return false;
+        return min_in && kk >= min_k && kk - min_k < 64 && (min_in >> (kk - min_k)) >= blt::kTokRange;
+    };
     for (int batch = 1;; batch = 4) {
         for (int b = 0; b < batch; ++b, ++k) {
-            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k};
+            const Chain c{tot + ((k - 1) & 1), tot + (k & 1), done, (uint32_t)k, scan_ok(k + 1)};
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
                 map_ready = false;
             }
-            const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
+            const bool scan = scan_ok(k);
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
                                   false, &c, scan, &map_ready))
                 return rc;
             cur ^= 1;
         }
         HIP_TRY(hipMemcpyAsync(rec, tot, 32, hipMemcpyDeviceToHost, s));
+        // the chunk offsets too when the next batch would leave the scan kernel by cs >> k alone
+        // (a few chunks: one more small copy in the same wait)
+        const bool rd_off = !scan_ok(k + 4) && L.nchunks >= 2 && L.nchunks <= 4096;
+        if (rd_off) {
+            hoff.resize(L.nchunks + 1);
+            HIP_TRY(hipMemcpyAsync(hoff.data(), off[cur], 8 * (L.nchunks + 1), hipMemcpyDeviceToHost, s));
+        }
         HIP_TRY(hipStreamSynchronize(s));
         if (int rc = chain_sticky(h, ws, L, k - 1 - k_idle)) return rc;
         if (fused && (rec[2] >> 32)) return fallback();
         if ((uint32_t)rec[2]) break;
+        if (rd_off) {   // pass k's input chunks, the last aside
+            uint64_t m = ~0ull;
+            for (uint64_t c = 0; c + 1 < L.nchunks; ++c) m = std::min(m, hoff[c + 1] >= hoff[c] ? hoff[c + 1] - hoff[c] : 0);
+            min_in = m;
+            min_k = k;
+        }
         if (k - k_idle > n + 8)
             return fail(BLT_E_IO, "general map: no fixpoint after %llu passes", (unsigned long long)(k - k_idle));
         // the last pass k - 1 left N tokens out of Nin (Nin unknown after the fused passes): the sparse
@@ -2001,6 +2053,8 @@ int blt_debug_set_pin_ring(int on) { return g_pin_ring.exchange(on ? 1 : 0) > 0 
 // Test hook: 0 runs every general map on the two-kernel chain, 1 (default) lets eligible maps fuse
 // passes 1 and 2.
 void blt_debug_set_fused(int on) { g_fused.store(on ? 1 : 0, std::memory_order_relaxed); }
+int blt_debug_set_u16_chain(int bits) { return g_u16_chain.exchange(bits); }
+int blt_debug_set_fused_only(int on) { return g_fused_only.exchange(on ? 1 : 0); }
 uint32_t blt_debug_last_fused() { return t_last_fused; }
 
 // Not in the public header: num_cpus::get() over a given cgroup root, /proc/self/cgroup file and
@@ -2019,6 +2073,9 @@ uint32_t blt_debug_set_inject(uint32_t bits) { return g_inject.exchange(bits); }
 // Not in the public header: the number of u16 passes the calling thread's last general-map
 // encode ran (the pass after which nothing can merge; later enqueued passes returned at once).
 uint32_t blt_debug_last_u16_passes(void) { return t_last_u16_passes; }
+// Not in the public header: u16 passes the calling thread's last general-map encode enqueued on the
+// scan kernel (done or not).
+uint32_t blt_debug_last_scan_passes(void) { return t_last_scan_passes; }
 
 // Not in the public header: a test hook that runs the kernels' device-error path (the one a
 // look-back timeout takes) for handle h on the current device and stream, setting error bit 1 in

@@ -1924,12 +1924,16 @@ constexpr uint32_t kCmStart = 1u << 11, kCmEnd = 1u << 23;
 // The next pass's chunk-map words for chunk c starting at output token P (round 6): the start in
 // P's wave range, the end of chunk c - 1 in the range of P - 1.  The two marks of one word can come
 // from two tiles on two XCDs: agent-scope ORs into a map zeroed one pass earlier.  (It replaces a
-// chunk_map_kernel launch per u16 pass, 4.8 us plus its launch gap on the chain row.)
-__device__ __forceinline__ void cm_mark(uint64_t* m, uint64_t P, uint32_t c) {
-    __hip_atomic_fetch_or(m + (P >> 10), (P & 1023u) | kCmStart | ((uint64_t)c << 32), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
-    if (c) __hip_atomic_fetch_or(m + ((P - 1) >> 10), (((P - 1) & 1023u) << 12) | kCmEnd, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+// chunk_map_kernel launch per u16 pass, 4.8 us plus its launch gap on the chain row.)  The host
+// asks for the map only when the next pass runs on this kernel, so its chunks hold kTokRange tokens
+// or more: a second start or end in one range is chunk_map_kernel's error 16 (host bug).
+__device__ __forceinline__ void cm_mark(const PassParams& p, uint64_t* m, uint64_t P, uint32_t c) {
+    const uint64_t o1 = __hip_atomic_fetch_or(m + (P >> 10), (P & 1023u) | kCmStart | ((uint64_t)c << 32),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t o2 = 0;
+    if (c) o2 = __hip_atomic_fetch_or(m + ((P - 1) >> 10), (((P - 1) & 1023u) << 12) | kCmEnd, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+    if ((o1 & kCmStart) || (o2 & kCmEnd)) flag_error(p.ctl, KARG(sticky), 16u);
 }
 
 __device__ __forceinline__ uint64_t token_count(const PassParams& p) {
@@ -2149,7 +2153,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
         // dense: every pair merges, so the only possible chunk start is the range's first token
         if (cstart && lane == 0) {
             KARG(chunk_off)[cwh] = O + goff;
-            if (inplace && p.cmap_next) cm_mark(p.cmap_next, O + goff, cwh);
+            if (inplace && p.cmap_next) cm_mark(p, p.cmap_next, O + goff, cwh);
         }
         emit_dense(st.v[j], cg, gb - (gb & ~15u), ro, gb & ~15u, lane);
         return;
@@ -2167,7 +2171,7 @@ __device__ __forceinline__ void emit_tok(const PassParams& p, uint64_t wtok, uin
         if (e < 16u) {
             const uint64_t P = O + goff + lane_off + __popc(L & ((1u << e) - 1u));
             KARG(chunk_off)[cwh] = P;
-            if (inplace && p.cmap_next) cm_mark(p.cmap_next, P, cwh);
+            if (inplace && p.cmap_next) cm_mark(p, p.cmap_next, P, cwh);
         }
     }
     const uint32_t wcnt = uni(lane_u32(lane_off + __popc(L), 63));
@@ -2361,6 +2365,12 @@ __device__ __forceinline__ void fused_front(const PassParams& p, uint32_t tab, u
                 C2 = (l2 && ((H2 >> lst) & 1ull)) ? 0u : 1u;
             }
         }
+        // A chunk start at byte wb + 1 whose byte wb merged into the halo's last token (C1 = 0) is the
+        // range's first first-pass token: the pair before it is cut in pass 2 as well, so it lands.
+        // (Round 6: the halo's pass-2 rule saw the pair as mergeable and gave C2 = 0; the range's
+        // count then disagreed with the carry the tile resolve gave its emission, and the next
+        // range's tokens overwrote its last one, in whichever order the waves stored.)
+        if (s == 1u && C1 == 0u) C2 = 1u;
         if (!ok) {   // no restart: this kernel cannot resolve the range (the host falls back)
             if (lane == 0) {
                 *KARG(fused_fail) = 1u;
@@ -2467,16 +2477,21 @@ __global__ __launch_bounds__(kThreads) void scan_tokens_kernel(PassParams p) {
         // previous pass read) are zeroed here over the live workgroups; this pass's own were zeroed by
         // the previous pass, or by chunk_map_kernel before the first.  No count-out at the end: the
         // next pass needs nothing from this one's tail.
+        // These stores run beside this pass's ticket atomics and status publishes, some on the same
+        // cache lines (the control block and the first status words share one): agent-scope
+        // stores, coherent with them, not plain stores into an XCD's L2.
         const uint64_t live = gridDim.x < ntiles ? gridDim.x : ntiles;
         if (p.cmap_zero) {
             const uint64_t nr = (n + kWavePos - 1) / kWavePos;
-            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < nr; i += live * kThreads) p.cmap_zero[i] = 0ull;
+            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < nr; i += live * kThreads)
+                __hip_atomic_store(p.cmap_zero + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (p.status_zero)
-            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < ntiles; i += live * kThreads) p.status_zero[i] = 0ull;
+            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < ntiles; i += live * kThreads)
+                __hip_atomic_store(p.status_zero + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (blockIdx.x == 0 && tid == 0) {
-            if (p.status_zero) p.ctl[p.tick ^ kCtlTickAlt] = 0u;
-            p.ctl[kCtlCover] = 0u;   // this pass dirties the status words
+            if (p.status_zero) __hip_atomic_store(p.ctl + (p.tick ^ kCtlTickAlt), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.ctl + kCtlCover, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // status words dirtied
         }
     }
     if (tid == 0) {

@@ -1308,3 +1308,147 @@ def test_sparse_list_rounds_across_the_bound():
     assert tok * 2 == exp.size
     assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
     assert np.array_equal(np.diff(d_off.cpu().numpy()) * 2, elens)
+
+
+CYCLIC_DENSE_MAP = {**{(32, c): 32 for c in range(97, 123)}, (300, 301): 302}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["long_chunks", "one_chunk_shrinks", "odd_cs"])
+def test_scan_kernel_past_the_static_bound(case):
+    """Round 6: the host keeps a general map's u16 passes on the scan kernel past the pass where
+    cs >> k falls below 1024 tokens, from the chunk offsets it reads at a batch end (a pass at most
+    halves a chunk).  Chunks that stay long (a cyclic map eating one letter per word and pass) keep
+    the scan kernel; a chunk of 'a's that halves every pass (a doubling chain beside the cyclic
+    map) sends the passes back to merge_tokens_kernel in time.  Bit-exact, host and device API,
+    device chunk offsets."""
+    import torch
+    L = blt_amd._lib.lib()
+    if case == "long_chunks":
+        m, cs = CYCLIC_DENSE_MAP, 1 << 16
+        data = synth.text(3 * (1 << 20) + 7, seed=41)
+    elif case == "odd_cs":
+        m, cs = CYCLIC_DENSE_MAP, 3 * (1 << 16) + 5
+        data = synth.text(5 * (1 << 20) + 1, seed=42)
+    else:
+        m = dict(CYCLIC_DENSE_MAP)
+        m.update(synth.doubling_chain(12))
+        cs = 1 << 16
+        data = synth.text(2 * (1 << 20) + 9, seed=43)
+        data[cs:2 * cs] = 97   # the second chunk: 64 Ki 'a', 32 Ki tokens after the byte pass, halving
+    exp, elens = O.COracle(m).run(data, cs, threads=16, return_lens=True)
+    s = blt_amd.BpeStrategy(m)
+    prev = _sparse(0)   # the full passes (the sparse passes would take a cyclic map's tail)
+    try:
+        got = s.process_chunks(data, cs)
+        scans_host = int(L.blt_debug_last_scan_passes())
+        n = data.size
+        nch = (n + cs - 1) // cs
+        d_in = torch.from_numpy(data).cuda()
+        d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+        d_off = torch.full((nch + 1,), -1, dtype=torch.int64, device="cuda")
+        wsb = s.workspace_size(n, cs)
+        ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream, d_off.data_ptr(),
+                              sync=True)
+        torch.cuda.synchronize()
+        passes = int(L.blt_debug_last_u16_passes())
+        scans = int(L.blt_debug_last_scan_passes())
+    finally:
+        _sparse(prev)
+    assert np.array_equal(got, exp)
+    assert tok * 2 == exp.size
+    assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp)
+    assert np.array_equal(np.diff(d_off.cpu().numpy()) * 2, elens)
+    static = max(k for k in range(1, 64) if (cs >> k) >= 1024)   # scan passes cs >> k alone allows
+    if case == "one_chunk_shrinks":
+        assert scans <= static + 5, (scans, static, passes)   # back to merge_tokens within a batch
+    else:
+        assert passes > static + 4, (passes, static)
+        assert scans > static + 4, (scans, static, passes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cs", [32768, 65536, 65536 + 4097])
+@pytest.mark.parametrize("mapname", ["doubling", "cyclic"])
+def test_scan_to_merge_transition_parity(mapname, cs):
+    """Round 6: the last u16 pass on the scan kernel before merge_tokens_kernel takes over, at odd and
+    even pass numbers (chained scan passes alternate status and ticket words by pass parity and
+    zero the next pass's), on a bounded chain (all passes enqueued) and a cyclic map (host-checked
+    batches); synchronous and asynchronous device calls, 0x5A-filled workspace."""
+    import torch
+    m = synth.doubling_chain(12) if mapname == "doubling" else CYCLIC_DENSE_MAP
+    data = synth.text(1 << 20, seed=44)
+    if mapname == "doubling":
+        data[::3] = 97
+        data[: 3 * cs // 2] = 97
+    exp = O.COracle(m).run(data, cs, threads=16)
+    s = blt_amd.BpeStrategy(m)
+    prev = _sparse(0)
+    try:
+        n = data.size
+        d_in = torch.from_numpy(data).cuda()
+        wsb = s.workspace_size(n, cs)
+        stream = torch.cuda.current_stream().cuda_stream
+        for sync in (True, False):
+            d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+            ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+            tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream, sync=sync)
+            torch.cuda.synchronize()
+            if sync:
+                assert tok * 2 == exp.size, (sync, tok, exp.size)
+            assert np.array_equal(d_out[:exp.size].cpu().numpy(), exp), sync
+    finally:
+        _sparse(prev)
+
+
+def _greedy_pass(m, toks):
+    """One greedy left-to-right pass of the reference's merge loop (tokenizer.rs:56-93)."""
+    out, i, n = [], 0, len(toks)
+    while i < n:
+        if i + 1 < n and (toks[i], toks[i + 1]) in m:
+            out.append(m[(toks[i], toks[i + 1])])
+            i += 2
+        else:
+            out.append(toks[i])
+            i += 1
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [44, 45])
+def test_fused_chunk_start_after_a_merged_first_byte(seed):
+    """Round 6: the fused kernel (u16 passes 1 and 2 in one launch), its output alone
+    (blt_debug_set_fused_only), against two greedy passes per chunk.  69,633-byte chunks put a
+    chunk start at byte 1 of a wave range; with ' ' + letter -> ' ' the range's byte 0 merges into
+    the halo's last token, so the chunk start is the range's first first-pass token and must land in
+    pass 2.  The halo rule gave it carry 0: the range's count was one short and the next range's
+    tokens overwrote its last one (every run: one token lost)."""
+    import torch
+    L = blt_amd._lib.lib()
+    m, cs = CYCLIC_DENSE_MAP, 65536 + 4097
+    data = synth.text(1 << 20, seed=seed)
+    n = data.size
+    exp = []
+    for c0 in range(0, n, cs):
+        exp += _greedy_pass(m, _greedy_pass(m, data[c0:c0 + cs].tolist()))
+    exp = np.array(exp, dtype=np.uint16)
+    s = blt_amd.BpeStrategy(m)
+    prev_sp, prev_f = _sparse(0), L.blt_debug_set_fused_only(1)
+    L.blt_debug_set_fused(1)
+    try:
+        d_in = torch.from_numpy(data).cuda()
+        d_out = torch.zeros(2 * n, dtype=torch.uint8, device="cuda")
+        wsb = s.workspace_size(n, cs)
+        ws = torch.full((wsb,), 0x5A, dtype=torch.uint8, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        tok = s.encode_device(d_in.data_ptr(), n, cs, d_out.data_ptr(), ws.data_ptr(), wsb, stream, sync=True)
+        torch.cuda.synchronize()
+        assert L.blt_debug_last_fused() == 1
+    finally:
+        _sparse(prev_sp)
+        L.blt_debug_set_fused_only(prev_f)
+    got = d_out[:2 * tok].cpu().numpy().view(">u2").astype(np.uint16)
+    assert tok == exp.size
+    assert np.array_equal(got, exp)
