@@ -720,20 +720,38 @@ struct Chain {
     bool next_scan = false;           // the next pass runs on the scan kernel too (it builds its chunk map)
 };
 
-// tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).  *map_ready (u16
-// passes of a chain): the previous pass was a scan pass, which built this pass's chunk map and reset
-// the status words; set for the next pass to whether this one was.
+// What the previous launch of a chain left for the next u16 pass (round 6).  Chained u16 passes
+// (scan or merge kernel) alternate two sets of look-back status words and ticket words; each pass
+// zeroes the other set for the pass after it, so only the first pass of a run needs the chunk-map
+// kernel (scan) or a memset (merge) to zero its own.  Any other kernel in between (the finish or
+// sparse kernels) resets it.
+struct U16Run {
+    bool map_ready = false;   // the previous pass was a scan pass that built this pass's chunk map
+    bool st_ready = false;    // the previous pass zeroed set `par`'s status words and ticket
+    uint32_t par = 0;         // the set this pass uses: 0 pass 1's status words and ctl[0], 1 the others
+    void reset() { map_ready = st_ready = false; }
+};
+
+// tok_scan: a u16 pass on the scan kernel (every chunk holds >= kTokRange tokens).  run (u16 passes
+// of a chain): see U16Run, updated for the next pass.
 int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8_t* ws, const WsLayout& L,
              const void* in, bool in_u16, uint64_t n, uint64_t cs, const uint64_t* cstart, void* out, bool be,
              uint64_t out_cap, uint64_t* chunk_off, bool ws_zeroed = false, const Chain* chain = nullptr,
-             bool tok_scan = false, bool* map_ready = nullptr) {
+             bool tok_scan = false, U16Run* run = nullptr) {
     const bool columnar = !in_u16 && cs >= blt::kMinChunkBytes && h->byte_mode >= 0 && be;   // byte-pass fast kernel
     const uint64_t tile = columnar ? blt::kTilePosBytes
                                    : in_u16 ? (tok_scan ? blt::kTilePosTok : blt::kTilePosU16) : blt::kTilePos;
     const uint64_t ntiles = (n + tile - 1) / tile;
     if (ntiles > 0xFFFFFFFFull) return fail(BLT_E_INVALID_INPUT, "input too large");
-    // (the u16 scan's chunk-map kernel zeroes the control block and status words itself)
-    if (!ws_zeroed && !(in_u16 && tok_scan)) HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
+    if (!(g_u16_chain.load(std::memory_order_relaxed) & 1)) run = nullptr;
+    const bool chained = in_u16 && chain && run;
+    // (the u16 scan's chunk-map kernel zeroes the control block and status words itself, and a
+    // chained pass finds them zeroed by the pass before it)
+    const bool merge_ready = chained && !tok_scan && run->st_ready;
+    if (!ws_zeroed && !(in_u16 && tok_scan) && !merge_ready) {
+        HIP_TRY(hipMemsetAsync(ws, 0, up16(blt::kCtlBytes + 8 * ntiles), s));
+        if (chained) run->par = 0;   // (the memset zeroed set 0: the control block and pass 1's words)
+    }
     blt::PassParams p{};
     p.in = in;
     p.n = n;
@@ -771,26 +789,25 @@ int run_pass(const blt_bpe* h, const DevTables* t, int dev, hipStream_t s, uint8
     p.inject = g_inject.load(std::memory_order_relaxed);
     p.sticky = h->sticky.load(std::memory_order_acquire);
     const bool scan16 = in_u16 && tok_scan;
-    if (!(g_u16_chain.load(std::memory_order_relaxed) & 1)) map_ready = nullptr;
-    const bool ready = scan16 && chain && map_ready && *map_ready;
-    if (scan16) {
-        const uint32_t r = chain ? chain->pass_id % 3u : 0u;
-        auto map = [&](uint32_t i) { return reinterpret_cast<uint64_t*>(ws + L.cmap + (uint64_t)(i % 3u) * L.cmap_stride); };
-        p.cmap = map(r);
-        if (chain && map_ready) {
-            // chained scan passes alternate status words and ticket words by pass parity; each
-            // zeroes the next pass's (whatever kernel runs it: a chunk-map or merge pass zeroes its own)
-            const bool odd = chain->pass_id & 1u;
-            p.status = reinterpret_cast<uint64_t*>(ws + (odd ? L.status2 : L.status));
-            p.status_zero = reinterpret_cast<uint64_t*>(ws + (odd ? L.status : L.status2));
-            p.tick = odd ? blt::kCtlTickAlt : 0u;
-            if (chain->next_scan) {   // the next pass's chunk map, built here
-                p.cmap_next = map(r + 1u);
-                p.cmap_zero = map(r + 2u);
-            }
+    const bool ready = scan16 && chained && run->map_ready;
+    auto map = [&](uint32_t i) { return reinterpret_cast<uint64_t*>(ws + L.cmap + (uint64_t)(i % 3u) * L.cmap_stride); };
+    const uint32_t r = chain ? chain->pass_id % 3u : 0u;
+    if (scan16) p.cmap = map(r);
+    if (chained) {
+        // this pass's set of status words and ticket, zeroed by the pass before it (or by the
+        // chunk-map kernel or the memset); the other set zeroed here for the next pass
+        const bool alt = run->par != 0;
+        p.status = reinterpret_cast<uint64_t*>(ws + (alt ? L.status2 : L.status));
+        p.status_zero = reinterpret_cast<uint64_t*>(ws + (alt ? L.status : L.status2));
+        p.tick = alt ? blt::kCtlTickAlt : 0u;
+        if (scan16 && chain->next_scan) {   // the next pass's chunk map, built here
+            p.cmap_next = map(r + 1u);
+            p.cmap_zero = map(r + 2u);
         }
+        run->par ^= 1u;
+        run->st_ready = true;
+        run->map_ready = scan16 && chain->next_scan;
     }
-    if (map_ready) *map_ready = scan16 && chain && chain->next_scan;
     p.ws_check = (ws_zeroed && !in_u16 && !chain) ? 1u : 0u;   // the caller's BLT_ENCODE_WORKSPACE_ZEROED
     if (columnar) HIP_TRY(blt::launch_scan_bytes(p, h->byte_mode, (chain && h->live_first) ? 1 : 0, dev, s));
     else if (scan16) {
@@ -1192,8 +1209,8 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
     };
     t_last_fused = fused ? 1 : 0;
     uint64_t rec[4] = {0, 0, 0, 0};
-    // the previous launch was a u16 scan pass: the next scan pass's chunk map is built (run_pass)
-    bool map_ready = false;
+    // what the previous launch left for the next u16 pass (run_pass)
+    U16Run u16run;
     // the finish kernels, once per encode: at the first u16 pass whose input chunks may fit in LDS
     bool fin_tried = !g_finish.load(std::memory_order_relaxed);
     auto finish_now = [&](uint64_t kk) {
@@ -1213,7 +1230,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
-                map_ready = false;
+                u16run.reset();
                 if (out_tokens) {
                     // a caller that waits anyway: see whether the finish ran (its gate word, the longest
                     // chunk, fit in LDS) before enqueueing the passes it turned into no-ops
@@ -1225,7 +1242,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             }
             const bool scan = k < 64 && (cs >> k) >= blt::kTokRange;
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
-                                  false, &c, scan, &map_ready))
+                                  false, &c, scan, &u16run))
                 return rc;
             cur ^= 1;
         }
@@ -1283,7 +1300,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
         if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), n, gate, k, off[cur], off[cur ^ 1],
                                 tot, &r))
             return rc;
-        map_ready = false;
+        u16run.reset();
         if (r.taken) {
             bool fin = false;
             if (int rc = sparse_taken(r, &fin)) return rc;
@@ -1313,11 +1330,11 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (finish_now(k)) {
                 if (int rc = run_finish(h, t, dev, s, ws, L, d_out, (uint32_t)k, off[cur], off[cur ^ 1], tot + (k & 1), done))
                     return rc;
-                map_ready = false;
+                u16run.reset();
             }
             const bool scan = scan_ok(k);
             if (int rc = run_pass(h, t, dev, s, ws, L, d_out, true, n, 0, off[cur], d_out, true, 2 * n, off[cur ^ 1],
-                                  false, &c, scan, &map_ready))
+                                  false, &c, scan, &u16run))
                 return rc;
             cur ^= 1;
         }
@@ -1352,7 +1369,7 @@ int encode_device(const blt_bpe* h, const uint8_t* d_in, uint64_t n, uint64_t cs
             if (int rc = run_sparse(h, t, dev, s, ws, L, d_out, tot + ((k - 1) & 1), N, nullptr, k, off[cur],
                                     off[cur ^ 1], tot, &r))
                 return rc;
-            map_ready = false;
+            u16run.reset();
             if (r.taken) {
                 bool fin = false;
                 if (int rc = sparse_taken(r, &fin)) return rc;

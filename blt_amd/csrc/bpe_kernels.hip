@@ -454,6 +454,15 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
         // the grid was sized for the input's bound; workgroups past the tiles there are leave
         // before copying the table (the ones below claim every ticket)
         if (blockIdx.x >= p.ntiles) return;
+        // chained u16 passes (round 6, as the scan kernel): the next pass's status words and ticket
+        // (the other set) zeroed here, with agent-scope stores beside this pass's ticket atomics
+        if (p.status_zero) {
+            const uint64_t live = gridDim.x < p.ntiles ? gridDim.x : p.ntiles;
+            for (uint64_t i = (uint64_t)blockIdx.x * kThreads + tid; i < p.ntiles; i += live * kThreads)
+                __hip_atomic_store(p.status_zero + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0 && tid == 0)
+                __hip_atomic_store(p.ctl + (p.tick ^ kCtlTickAlt), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     const uint32_t cover = kDense ? ws_cover(p) : 0xFFFFFFFFu;
     const InT* in = reinterpret_cast<const InT*>(p.in);
@@ -470,7 +479,7 @@ __device__ __forceinline__ void merge_pass_body(const PassParams& pin) {
     const bool refused = kDense && ws_refused(p, p.ntiles, cover);
     for (;;) {
         if (refused) break;
-        if (tid == 0) s_ticket = atomicAdd(p.ctl, 1u);
+        if (tid == 0) s_ticket = atomicAdd(p.ctl + p.tick, 1u);
         __syncthreads();
         const uint32_t T = s_ticket;
         if (T >= p.ntiles) break;
