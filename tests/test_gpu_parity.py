@@ -1518,4 +1518,5 @@ def test_fused_random_maps_against_two_passes():
     finally:
         _sparse(prev_sp)
         L.blt_debug_set_fused_only(prev_f)
-    assert ran >= 5, ran   # (7 of the 24 with this seed: the rest are single-pass maps or fall back)
+    assert ran >= 5, ran   # (7 of the 24 with this seed; the others take another path: single-pass or
+    #  byte-pair-key maps, halo fallbacks)
