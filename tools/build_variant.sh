@@ -11,7 +11,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result"
 mkdir -p "$R/build/exp"
-$HIPCC $HF $FLAGS -x hip -c "$R/blt_amd/csrc/blt_host.cpp" -o "$R/build/exp/h_$NAME.o" &
+$HIPCC $HF $FLAGS -x hip -I"$R/blt_amd/csrc" -c "${HSRC:-$R/blt_amd/csrc/blt_host.cpp}" -o "$R/build/exp/h_$NAME.o" &
 $HIPCC $HF $FLAGS -x hip -c "$R/blt_amd/csrc/blt_pipeline.cpp" -o "$R/build/exp/p_$NAME.o" &
 $HIPCC $HF $FLAGS ${KFLAGS:-} -I"$R/blt_amd/csrc" -c "${KSRC:-$R/blt_amd/csrc/bpe_kernels.hip}" -o "$R/build/exp/k_$NAME.o"
 wait
