@@ -4006,13 +4006,15 @@ static bool sparse_ok(const SparseParams& q) {
 }
 hipError_t launch_sparse_detect(const SparseParams& q, hipStream_t s) {
     if (!sparse_ok(q)) return hipErrorInvalidValue;
-    // a lane per 32 positions; every position in one wave of workgroups when the table is small
-    // (each workgroup stages it), else a grid of 2048 looping.  (A workgroup per list workgroup's
-    // words, 16 rounds each, measured 240 us against 142 on selfval.)
+    // a lane per 32 positions; a grid of at most 8192 workgroups looping when the table is small
+    // (each workgroup stages it), else 2048.  (selfval, 33 K workgroups of one round each: 145-148 us;
+    // 8192: 134, 6144: 137, 12288: 135, 16384: 135, 4096: 143, 2048: 172, round 6, r06ac/r06ad.  A
+    // workgroup per list workgroup's words, 16 rounds each, measured 240 us against 142.)
     const uint64_t nwords = (q.n + 31) / 32;
     uint64_t blocks = (nwords + 255) / 256;
     const bool lds = q.hbytes && q.hbytes <= kHashLdsMax;
-    if (blocks > 2048 && !(lds && q.hbytes <= 4096)) blocks = 2048;
+    const uint64_t max_blocks = (lds && q.hbytes <= 4096) ? 8192 : 2048;
+    if (blocks > max_blocks) blocks = max_blocks;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(sparse_sample_kernel, dim3(kSparseSampleBlocks), dim3(1024), 0, s, q);
     const size_t smem = (lds ? ((q.hbytes + 15u) & ~15u) : 0u) + (q.nchunks <= kDetectCsLds ? 8 * q.nchunks : 0);
