@@ -659,7 +659,7 @@ WsLayout ws_layout(const blt_bpe* h, uint64_t n, uint64_t cs) {
     L.cmap = up256(L.off_b + up16(8 * (L.nchunks + 1)));
     L.cmap_stride = up256(8 * ((n + blt::kTokRange - 1) / blt::kTokRange));
     L.gstat = L.cmap + 3 * L.cmap_stride;   // finish: a status word per group
-    // odd chained u16 scan passes' status words (even ones use pass 1's)
+    // the second set of look-back status words of chained u16 passes (U16Run; the first is pass 1's)
     L.status2 = up256(L.gstat + up16(8 * L.nchunks));
     L.bytes = single_pass ? L.cmap : L.status2 + up16(8 * L.ntiles);
     if (!single_pass && !chain_bounded(h) && n < (1ull << 32)) {
